@@ -1,0 +1,119 @@
+/*
+ * wbq_oracle.h -- CPU restatement (TEST INFRASTRUCTURE ONLY) of the per-tick
+ * torque solve that ADVRHumanoids/qppvm's QPPVMPlugin delegates to
+ * OpenSoT + qpOASES.
+ *
+ * This is the *checker*: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it. The product path (qppvm_amd, libwbq.so) never
+ * links or calls it.
+ *
+ * Parity status: the reference cannot be built or run anywhere in this
+ * pipeline (OpenSoT, qpOASES, XBotInterface, XCM, Eigen are absent; SURVEY.md
+ * 8c), and the reference holds no tests or golden data. The oracle is
+ * therefore pinned to closed-form known-answer tests and to an independent
+ * numpy/scipy restatement (tests/golden/make_golden.py), NOT to reference
+ * outputs: "parity unpinned" against the reference binaries.
+ *
+ * The formulation deliberately follows the reference's *task* form (x-space,
+ * A = J M^-1 formed explicitly, H = A^T W A, qpOASES-style primal active set)
+ * so that it is an independent computation path from the GPU kernels, which
+ * work in the transformed u = M^-1 x space with a dual active-set method.
+ *
+ * Reference anchors (files under /root/reference):
+ *   src/QPPVMPlugin.cpp:56-67    effort limits, tau_min = -tau_max, bounds shifted by -h
+ *   src/QPPVMPlugin.cpp:99-118   joint impedance task K=5, D=2, useInertiaMatrix(true)
+ *   src/QPPVMPlugin.cpp:129-152  two Cartesian impedance tasks Kc=700, Dc=70, rows {0,1,2}
+ *   src/QPPVMPlugin.cpp:177-179  stack ((ee_right + ee_left) / joint_task) << torque_limits
+ *   src/QPPVMPlugin.cpp:188      QPOases_sot(stack, bounds, eps_regularisation = 1.0)
+ *   src/QPPVMPlugin.cpp:203-205  bounds re-shifted each tick
+ *   src/QPPVMPlugin.cpp:246-256  solve; on failure tau_qp = 0; tau = tau_qp + h
+ */
+#ifndef WBQ_ORACLE_H
+#define WBQ_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WBQ_REF_MAX_TASKS 4
+
+/* select_mode: how OpenSoT::Indices::range(0,2) (QPPVMPlugin.cpp:134,147) restricts
+ * a 6-D Cartesian impedance task.  [upstream semantics unverifiable offline]
+ *   0 = SUBTASK: the full 6-D task (A6, b6) is built, then rows are selected
+ *       (OpenSoT SubTask semantics).
+ *   1 = TASK:    the task-space force F is masked before J^T F. */
+#define WBQ_REF_SELECT_SUBTASK 0
+#define WBQ_REF_SELECT_TASK 1
+
+/* joint_weight: weight of the joint impedance task on level 1 (W1). */
+#define WBQ_REF_WEIGHT_IDENTITY 0
+#define WBQ_REF_WEIGHT_INERTIA 1
+
+/* statuses (shared with the product ABI, include/wbq.h) */
+#define WBQ_REF_OK 0
+#define WBQ_REF_MAXITER 1
+#define WBQ_REF_INFEASIBLE 2
+#define WBQ_REF_NUMERICAL 3
+
+typedef struct {
+    int n;                           /* joint DoF */
+    int ntasks;                      /* Cartesian tasks summed on level 0 */
+    int row_mask[WBQ_REF_MAX_TASKS]; /* bit r keeps row r of task t (reference: 0x7) */
+    int select_mode;                 /* WBQ_REF_SELECT_* */
+    int joint_weight;                /* WBQ_REF_WEIGHT_* */
+    const double *Kc;                /* [ntasks][6] diagonal Cartesian stiffness */
+    const double *Dc;                /* [ntasks][6] diagonal Cartesian damping */
+    const double *Kq;                /* [n] joint stiffness */
+    const double *Dq;                /* [n] joint damping */
+    const double *tau_max;           /* [n] */
+    const double *tau_min;           /* [n] */
+} wbq_ref_desc;
+
+/* One instance (all row-major fp64):
+ *   M [n][n] SPD inertia, J [ntasks][6][n] geometric Jacobians (linear rows 0-2,
+ *   angular 3-5), pose / pose_ref [ntasks][12] = [R | p] as 3x4 row-major,
+ *   q, qd, qref, h [n]. */
+typedef struct {
+    const double *M, *J, *pose, *pose_ref, *q, *qd, *qref, *h;
+} wbq_ref_instance;
+
+/* Cartesian error e = [p_ref - p ; vec(quat(R_ref R^T)) with w >= 0]. */
+void wbq_ref_cart_error(const double pose[12], const double pose_ref[12], double e[6]);
+
+/* Builds the two levels exactly as the OpenSoT tasks would (x = tau - h):
+ *   A0 [m0][n], b0 [m0]   level 0: stacked Cartesian tasks  A = S J M^-1, b = S J M^-1 J^T F
+ *   H1 [n][n], g1 [n]     level 1: joint task A1 = M^-1, b1 = M^-1 tau_imp, H1 = A1^T W A1, g1 = -A1^T W b1
+ *   lb, ub [n]            torque limits shifted by -h
+ * Returns m0 (>0) or -WBQ_REF_NUMERICAL when M is not SPD. */
+int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *A0, double *b0,
+                     double *H1, double *g1, double *lb, double *ub);
+
+/* Level 0: bounded least squares min 0.5||A x - b||^2, lb <= x <= ub (Stark-Parker BVLS with
+ * minimum-norm free-set solves). state[n] in/out: 0 free, -1 at lb, +1 at ub (warm start).
+ * Returns a WBQ_REF_* status. */
+int wbq_ref_level0(int m, int n, const double *A, const double *b, const double *lb,
+                   const double *ub, double *x, int *state, int *iters);
+
+/* Level 1: strictly convex QP min 0.5 x^T H x + g^T x s.t. Aeq x = beq, lb <= x <= ub,
+ * primal active set (qpOASES family) started from a feasible x with bound state[n]. */
+int wbq_ref_level1(int n, const double *H, const double *g, int me, const double *Aeq,
+                   const double *beq, const double *lb, const double *ub, double *x, int *state,
+                   int *iters);
+
+/* Whole per-tick chain for one instance: tau = x* + h (x* = 0 on failure, QPPVMPlugin.cpp:246-256).
+ * y0 (optional, [m0]) receives A0 x0*. Returns a WBQ_REF_* status. */
+int wbq_ref_qppvm_one(const wbq_ref_desc *d, const wbq_ref_instance *in, double *tau, double *y0,
+                      int *iters);
+
+/* Batched driver over contiguous instance arrays (strides implied by n, ntasks). */
+void wbq_ref_qppvm_batch(const wbq_ref_desc *d, int B, const double *M, const double *J,
+                         const double *pose, const double *pose_ref, const double *q,
+                         const double *qd, const double *qref, const double *h, double *tau,
+                         int32_t *status, int32_t *iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,129 @@
+"""Host-side problem descriptor for the QPPVM torque solve.
+
+Mirrors the configuration that ``demo::QPPVMPlugin::init_control_plugin`` wires into
+OpenSoT (reference ``src/QPPVMPlugin.cpp``):
+
+* level 0 = ``ee_task_right + ee_task_left`` (summed Cartesian impedance tasks,
+  ``:129-152``, ``:177``), gains ``Kc = 700 I6``, ``Dc = 70 I6`` (``:136-137``,
+  ``:148-149``), rows ``OpenSoT::Indices::range(0,2)`` (``:134``, ``:147``),
+  ``useInertiaMatrix(true)`` (``:139``, ``:151``);
+* level 1 = ``joint_task`` (``:114-118``), ``K = 5 I``, ``D = 2 I`` (``:105-106``);
+* global bounds = ``TorqueLimits(tau_max - h, tau_min - h)`` with
+  ``tau_min = -tau_max`` (``:56-58``, ``:66-67``, ``:112``, ``:203-205``);
+* solver = ``QPOases_sot(stack, bounds, eps_regularisation = 1.0)`` (``:188``).
+
+The structure is static per controller (it is the "AutoStack" of the reference);
+only per-tick numbers travel to the device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+SELECT_SUBTASK = 0  # full 6-D task built, then rows selected (OpenSoT SubTask semantics)
+SELECT_TASK = 1  # task-space force masked before J^T F
+
+WEIGHT_IDENTITY = 0  # joint task weight W1 = I
+WEIGHT_INERTIA = 1  # joint task weight W1 = M
+
+STATUS_OK = 0
+STATUS_MAXITER = 1
+STATUS_INFEASIBLE = 2
+STATUS_NUMERICAL = 3
+
+STATUS_NAMES = {0: "ok", 1: "max-iterations", 2: "infeasible", 3: "numerical"}
+
+
+def _vec(x, n, name):
+    a = np.asarray(x, dtype=np.float64)
+    if a.ndim == 0:
+        a = np.full(n, float(a))
+    if a.shape != (n,):
+        raise ValueError(f"{name} must have shape ({n},), got {a.shape}")
+    return np.ascontiguousarray(a)
+
+
+@dataclass
+class QPPVMProblem:
+    """Batch-shared structure + gains of the QPPVM stack.
+
+    Defaults are the reference literals (QPPVMPlugin.cpp); ``tau_max`` defaults to
+    150 N m per joint because the CENTAURO effort limits (URDF) are not in the
+    container.
+    """
+
+    n: int
+    ntasks: int = 2
+    row_mask: tuple = (0x7, 0x7)
+    select_mode: int = SELECT_SUBTASK
+    joint_weight: int = WEIGHT_IDENTITY
+    Kc: np.ndarray | float = 700.0
+    Dc: np.ndarray | float = 70.0
+    Kq: np.ndarray | float = 5.0
+    Dq: np.ndarray | float = 2.0
+    tau_max: np.ndarray | float = 150.0
+    tau_min: np.ndarray | float | None = None
+    max_iter: int = 0  # 0 = default cap (4 n + 32 active-set steps)
+    extra: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        n, T = int(self.n), int(self.ntasks)
+        if not (1 <= n <= 64):
+            raise ValueError("n must be in [1, 64]")
+        if not (1 <= T <= 4):
+            raise ValueError("ntasks must be in [1, 4]")
+        self.n, self.ntasks = n, T
+        rm = tuple(int(m) for m in self.row_mask)
+        if len(rm) == 1 and T > 1:
+            rm = rm * T
+        if len(rm) != T or any(not (0 < m < 64) for m in rm):
+            raise ValueError("row_mask needs one non-empty 6-bit mask per task")
+        self.row_mask = rm
+        kc = np.asarray(self.Kc, dtype=np.float64)
+        dc = np.asarray(self.Dc, dtype=np.float64)
+        self.Kc = np.ascontiguousarray(np.broadcast_to(kc, (T, 6)).astype(np.float64))
+        self.Dc = np.ascontiguousarray(np.broadcast_to(dc, (T, 6)).astype(np.float64))
+        self.Kq = _vec(self.Kq, n, "Kq")
+        self.Dq = _vec(self.Dq, n, "Dq")
+        self.tau_max = _vec(self.tau_max, n, "tau_max")
+        self.tau_min = -self.tau_max if self.tau_min is None else _vec(self.tau_min, n, "tau_min")
+        if self.select_mode not in (SELECT_SUBTASK, SELECT_TASK):
+            raise ValueError("select_mode must be SELECT_SUBTASK or SELECT_TASK")
+        if self.joint_weight not in (WEIGHT_IDENTITY, WEIGHT_INERTIA):
+            raise ValueError("joint_weight must be WEIGHT_IDENTITY or WEIGHT_INERTIA")
+
+    @property
+    def m0(self) -> int:
+        """Rows of level 0 (sum of selected task rows)."""
+        return sum(bin(m).count("1") for m in self.row_mask)
+
+
+# per-instance input arrays and their shapes (B = batch)
+INPUT_FIELDS = ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")
+
+
+def input_shapes(prob: QPPVMProblem, B: int) -> dict:
+    n, T = prob.n, prob.ntasks
+    return {
+        "M": (B, n, n),
+        "J": (B, T, 6, n),
+        "pose": (B, T, 12),
+        "pose_ref": (B, T, 12),
+        "q": (B, n),
+        "qd": (B, n),
+        "qref": (B, n),
+        "h": (B, n),
+    }
+
+
+def check_inputs(prob: QPPVMProblem, inputs: dict) -> int:
+    """Validate shapes/dtypes of a batch; returns B. Raises ValueError like the C ABI."""
+    B = int(np.asarray(inputs["h"]).shape[0])
+    for k, shp in input_shapes(prob, B).items():
+        a = inputs[k]
+        if tuple(a.shape) != shp:
+            raise ValueError(f"input {k}: expected shape {shp}, got {tuple(a.shape)}")
+        if a.dtype != np.float64:
+            raise ValueError(f"input {k}: expected float64, got {a.dtype}")
+    return B

@@ -1,0 +1,85 @@
+"""Synthetic randomized robot states (no URDF/checkpoints in the container).
+
+* M = Q diag(lam) Q^T, Q Haar-orthogonal, lam log-uniform in [1e-2, 1e1]  (cond 1e3)
+* J ~ N(0, 0.5^2) per task (6 x n)
+* q, q_ref ~ U(-pi, pi), qd ~ N(0, 1), h ~ N(0, 10^2)
+* poses: R Haar, p ~ U(-1, 1); reference = pose perturbed by N(0, 0.05^2) in
+  position and by a rotation vector ~ N(0, 0.05^2)
+Counter-based RNG (numpy Philox) keyed by ``seed``; ``offset`` skips instances so a
+shard on rank r reproduces exactly the rows [offset, offset+B) of the global batch.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .problem import QPPVMProblem
+
+
+def _rng(seed: int, stream: int) -> np.random.Generator:
+    return np.random.Generator(np.random.Philox(key=[int(seed) & 0xFFFFFFFFFFFFFFFF, int(stream)]))
+
+
+def _haar(rng, B, n):
+    Z = rng.standard_normal((B, n, n))
+    Q, R = np.linalg.qr(Z)
+    d = np.sign(np.diagonal(R, axis1=1, axis2=2))
+    d[d == 0] = 1.0
+    return Q * d[:, None, :]
+
+
+def _rotvec_to_R(w):
+    th = np.linalg.norm(w, axis=-1, keepdims=True)
+    k = np.where(th > 0, w / np.where(th > 0, th, 1.0), 0.0)
+    K = np.zeros(w.shape[:-1] + (3, 3))
+    K[..., 0, 1], K[..., 0, 2] = -k[..., 2], k[..., 1]
+    K[..., 1, 0], K[..., 1, 2] = k[..., 2], -k[..., 0]
+    K[..., 2, 0], K[..., 2, 1] = -k[..., 1], k[..., 0]
+    s, c = np.sin(th)[..., None], np.cos(th)[..., None]
+    eye = np.broadcast_to(np.eye(3), K.shape)
+    return eye + s * K + (1 - c) * (K @ K)
+
+
+def _pose(R, p):
+    out = np.zeros(R.shape[:-2] + (3, 4))
+    out[..., :3] = R
+    out[..., 3] = p
+    return out.reshape(R.shape[:-2] + (12,))
+
+
+def qppvm_instances(prob: QPPVMProblem, B: int, seed: int = 0, offset: int = 0,
+                    cond_max: float = 1e3) -> dict:
+    """B independent random instances (rows [offset, offset+B) of stream ``seed``)."""
+    n, T = prob.n, prob.ntasks
+    out = {k: [] for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
+    # generate in chunks keyed by absolute chunk index so offsets are reproducible
+    CH = 256
+    first, last = offset // CH, (offset + B - 1) // CH if B > 0 else -1
+    for c in range(first, last + 1):
+        rng = _rng(seed, c)
+        Q = _haar(rng, CH, n)
+        lam = np.exp(rng.uniform(np.log(1e-2), np.log(1e-2 * cond_max), (CH, n)))
+        M = (Q * lam[:, None, :]) @ Q.transpose(0, 2, 1)
+        M = 0.5 * (M + M.transpose(0, 2, 1))
+        J = rng.normal(0.0, 0.5, (CH, T, 6, n))
+        R = _haar(rng, CH * T, 3).reshape(CH, T, 3, 3)
+        det = np.linalg.det(R)
+        R[det < 0, :, 0] *= -1.0
+        p = rng.uniform(-1.0, 1.0, (CH, T, 3))
+        Rref = _rotvec_to_R(rng.normal(0.0, 0.05, (CH, T, 3))) @ R
+        pref = p + rng.normal(0.0, 0.05, (CH, T, 3))
+        q = rng.uniform(-np.pi, np.pi, (CH, n))
+        qref = rng.uniform(-np.pi, np.pi, (CH, n))
+        qd = rng.normal(0.0, 1.0, (CH, n))
+        h = rng.normal(0.0, 10.0, (CH, n))
+        lo = max(offset, c * CH) - c * CH
+        hi = min(offset + B, (c + 1) * CH) - c * CH
+        for k, v in (("M", M), ("J", J), ("pose", _pose(R, p)), ("pose_ref", _pose(Rref, pref)),
+                     ("q", q), ("qd", qd), ("qref", qref), ("h", h)):
+            out[k].append(v[lo:hi])
+    return {k: np.ascontiguousarray(np.concatenate(v, axis=0)) if v else
+            np.zeros((0,)) for k, v in out.items()}
+
+
+def replicate(inputs: dict, B: int) -> dict:
+    """Config 1: B identical copies of instance 0."""
+    return {k: np.ascontiguousarray(np.broadcast_to(v[:1], (B,) + v.shape[1:])) for k, v in inputs.items()}

@@ -1,0 +1,46 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+INPUT_KEYS = ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+def load_golden(n):
+    """Yield (group, QPPVMProblem, inputs, expected dict) from tests/golden/qppvm_n{n}.npz."""
+    from qppvm_amd.problem import QPPVMProblem
+    z = np.load(os.path.join(GOLDEN, f"qppvm_n{n}.npz"))
+    for g in z["groups"]:
+        g = str(g)
+        pre = g + "__"
+        prob = QPPVMProblem(n=n, tau_max=z[pre + "tau_max"],
+                            select_mode=int(z[pre + "select_mode"]),
+                            joint_weight=int(z[pre + "joint_weight"]),
+                            row_mask=tuple(int(m) for m in z[pre + "row_mask"]))
+        inp = {k: np.ascontiguousarray(z[pre + k]) for k in INPUT_KEYS}
+        exp = {k: z[pre + k] for k in ("tau", "y0", "status", "kat") if pre + k in z}
+        yield g, prob, inp, exp
+
+
+def rel_err(a, b):
+    """max_i ||a_i - b_i||_inf / max(1, ||b_i||_inf) over a batch."""
+    a = np.atleast_2d(a)
+    b = np.atleast_2d(b)
+    return float((np.abs(a - b).max(axis=1) / np.maximum(1.0, np.abs(b).max(axis=1))).max())
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    import oracle
+    oracle.build()
+    return oracle
