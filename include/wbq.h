@@ -1,0 +1,123 @@
+/*
+ * wbq.h -- C ABI of the MI355X batched whole-body-QP engine (libwbq.so).
+ *
+ * Drop-in boundary for the per-tick torque solve of ADVRHumanoids/qppvm's XBot RT
+ * plugins. The plugins keep their XBot surface; what they delegated to OpenSoT
+ * (task assembly, AutoStack, QPOases_sot) and qpOASES is replaced by these calls,
+ * batched over B robot instances / MPC rollouts. Entry points and the reference
+ * interface each one replaces:
+ *
+ *   wbq_create        <- QPPVMPlugin::init_control_plugin's task/stack/solver wiring
+ *                        (src/QPPVMPlugin.cpp:99-189: TorqueLimits :112,
+ *                        JointImpedanceCtrl :114-118, CartesianImpedanceCtrl :129-152,
+ *                        AutoStack :177-179, QPOases_sot(.., 1.0) :188).
+ *                        All device memory is allocated here (the reference sizes its
+ *                        Eigen buffers at init, :56-62), so wbq_solve never allocates.
+ *   wbq_set_inputs    <- the per-tick model pulls inside autostack->update(q)
+ *                        (:226; J, M, poses, qdot) plus h (:312), q_ref (:279) and the
+ *                        torque-limit shift (:203-205).
+ *   wbq_solve         <- solver->solve(tau_d) (:246) + tau_d = tau_qp + h (:256), for
+ *                        the whole batch, asynchronously on the context's HIP stream.
+ *   wbq_get_outputs   <- the tau_d handed to model->setJointEffort (:318) and the
+ *                        bool of solve() (:246) as a per-instance status.
+ *   wbq_reset_warmstart <- qpOASES hot-start state reset (QPOases_sot re-init) [upstream].
+ *   wbq_destroy       <- plugin close()/destructor (:339-342).
+ *
+ * Conventions: fp64, row-major, instance-major contiguous arrays:
+ *   M [B][n][n] SPD joint-space inertia        J [B][ntasks][6][n] (rows 0-2 linear, 3-5 angular)
+ *   pose, pose_ref [B][ntasks][12] = [R | p] 3x4 row-major (Eigen::Affine3d::matrix() top rows)
+ *   q, qd, qref, h [B][n]                       tau [B][n] out, status/iters [B] out
+ * Per-instance status: 0 ok, 1 iteration cap, 2 infeasible, 3 numerical. On status != 0
+ * tau = h (the reference's "SOLVER ERROR!" fallback tau_qp = 0, QPPVMPlugin.cpp:246-249).
+ * A context is not thread-safe: one context per caller thread, one HIP stream per context.
+ */
+#ifndef WBQ_H
+#define WBQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* API return codes */
+#define WBQ_SUCCESS 0
+#define WBQ_E_INVALID (-1)
+#define WBQ_E_DEVICE (-2)
+#define WBQ_E_UNSUPPORTED (-3)
+#define WBQ_E_CAPACITY (-4)
+
+/* per-instance statuses */
+#define WBQ_STATUS_OK 0
+#define WBQ_STATUS_MAXITER 1
+#define WBQ_STATUS_INFEASIBLE 2
+#define WBQ_STATUS_NUMERICAL 3
+
+/* problem forms */
+#define WBQ_FORM_QPPVM 0 /* QPPVMPlugin: 2-level torque-space impedance QP */
+
+/* Cartesian row selection semantics of OpenSoT::Indices::range(0,2) (QPPVMPlugin.cpp:134) */
+#define WBQ_SELECT_SUBTASK 0 /* full 6-D task built, rows selected afterwards */
+#define WBQ_SELECT_TASK 1    /* task-space force masked before J^T F */
+
+/* joint-task weight on level 1 */
+#define WBQ_WEIGHT_IDENTITY 0
+#define WBQ_WEIGHT_INERTIA 1
+
+/* memory kinds for wbq_inputs.memory */
+#define WBQ_MEM_HOST 0   /* copied (async H2D) into context-owned device buffers */
+#define WBQ_MEM_DEVICE 1 /* device pointers adopted as-is (caller keeps them alive) */
+
+typedef struct wbq_ctx wbq_ctx;
+
+typedef struct {
+    int form;          /* WBQ_FORM_* */
+    int n;             /* joint DoF, 1..64 */
+    int ntasks;        /* Cartesian tasks summed on level 0, 1..4 (reference: 2) */
+    int row_mask[4];   /* per task, bit r keeps task row r (reference: 0x7) */
+    int select_mode;   /* WBQ_SELECT_* */
+    int joint_weight;  /* WBQ_WEIGHT_* */
+    int max_batch;     /* capacity; every buffer is sized for it in wbq_create */
+    int max_iter;      /* active-set step cap per instance, 0 = default (4 n + 32) */
+    const double *Kc;  /* [ntasks][6] Cartesian stiffness diagonal (reference 700) */
+    const double *Dc;  /* [ntasks][6] Cartesian damping diagonal (reference 70) */
+    const double *Kq;  /* [n] joint stiffness (reference 5) */
+    const double *Dq;  /* [n] joint damping (reference 2) */
+    const double *tau_max; /* [n] effort limits */
+    const double *tau_min; /* [n] (reference: -tau_max, QPPVMPlugin.cpp:58) */
+} wbq_desc;
+
+typedef struct {
+    int batch;  /* B <= max_batch */
+    int memory; /* WBQ_MEM_* */
+    const double *M, *J, *pose, *pose_ref, *q, *qd, *qref, *h;
+} wbq_inputs;
+
+int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out);
+/* Launch on a caller-provided hipStream_t (NULL = the context's own stream). */
+int wbq_set_stream(wbq_ctx *ctx, void *hip_stream);
+int wbq_set_inputs(wbq_ctx *ctx, const wbq_inputs *in);
+int wbq_solve(wbq_ctx *ctx);
+int wbq_sync(wbq_ctx *ctx);
+/* Synchronous copy of the last solve's outputs to host memory (any pointer may be NULL). */
+int wbq_get_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
+/* Write outputs into caller-owned device buffers ([batch][n] / [batch]) instead of the
+ * context's (any NULL pointer reverts that output to the context buffer). */
+int wbq_set_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
+/* Device-resident outputs of the last solve (valid until the next wbq_solve/destroy). */
+int wbq_get_device_outputs(wbq_ctx *ctx, const double **tau, const int32_t **status,
+                           const int32_t **iters);
+/* Drop the warm-start working set of instances with mask[b] != 0 (NULL = all). */
+int wbq_reset_warmstart(wbq_ctx *ctx, const uint8_t *mask);
+/* Kernel timing with HIP events on the launch stream: enable, then read the summed
+ * device time (ms) and the number of timed launches since the last read. */
+int wbq_set_timing(wbq_ctx *ctx, int enable);
+int wbq_get_timing(wbq_ctx *ctx, double *total_ms, int *launches);
+void wbq_destroy(wbq_ctx *ctx);
+const char *wbq_last_error(const wbq_ctx *ctx);
+const char *wbq_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,317 @@
+// wbq_api.hip -- C ABI of libwbq (declared in include/wbq.h).
+//
+// The context owns every device buffer (allocated once in wbq_create, the analogue of
+// QPPVMPlugin::init_control_plugin sizing its Eigen buffers, src/QPPVMPlugin.cpp:56-62),
+// so wbq_solve is allocation-free and can be captured in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wbq.h"
+#include "wbq_kernels.h"
+
+struct wbq_ctx {
+    int device = 0;
+    wbq_desc d{};
+    int m0 = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // batch-shared parameters (device)
+    double *Kc = nullptr, *Dc = nullptr, *Kq = nullptr, *Dq = nullptr, *tmax = nullptr, *tmin = nullptr;
+    int *row_sel = nullptr;
+    // owned input buffers (capacity max_batch) and the pointers the next solve reads
+    double *own[8] = {};
+    const double *in[8] = {};
+    int batch = 0;
+    bool have_inputs = false;
+    // outputs: context-owned buffers and the ones the next solve writes
+    double *tau = nullptr;
+    int *status = nullptr;
+    int *iters = nullptr;
+    double *out_tau = nullptr;
+    int *out_status = nullptr;
+    int *out_iters = nullptr;
+    // event timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;  // pairs
+    int ev_used = 0;
+    double t_acc_ms = 0.0;
+    int t_launches = 0;
+    std::string err;
+};
+
+namespace {
+
+const char *kVersion = "wbq 0.1.0 (gfx950, fp64, QPPVM form)";
+
+size_t field_elems(const wbq_desc &d, int f)
+{
+    const size_t n = (size_t)d.n, T = (size_t)d.ntasks;
+    switch (f) {
+    case 0: return n * n;      // M
+    case 1: return T * 6 * n;  // J
+    case 2: return T * 12;     // pose
+    case 3: return T * 12;     // pose_ref
+    default: return n;         // q, qd, qref, h
+    }
+}
+
+int fail(wbq_ctx *c, int code, const std::string &msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(wbq_ctx *c, hipError_t e, const char *what)
+{
+    return fail(c, WBQ_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define WBQ_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+const char *wbq_version(void) { return kVersion; }
+
+const char *wbq_last_error(const wbq_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
+{
+    if (!out || !desc) return WBQ_E_INVALID;
+    *out = nullptr;
+    const wbq_desc &d = *desc;
+    if (d.form != WBQ_FORM_QPPVM) return WBQ_E_UNSUPPORTED;
+    if (d.n < 1 || d.n > 64 || d.ntasks < 1 || d.ntasks > wbq::kTMax || d.max_batch < 1)
+        return WBQ_E_INVALID;
+    if (d.select_mode != WBQ_SELECT_SUBTASK && d.select_mode != WBQ_SELECT_TASK) return WBQ_E_INVALID;
+    if (d.joint_weight != WBQ_WEIGHT_IDENTITY) return WBQ_E_UNSUPPORTED;  // W1 = M: CPU oracle only (yet)
+    if (!d.Kc || !d.Dc || !d.Kq || !d.Dq || !d.tau_max || !d.tau_min) return WBQ_E_INVALID;
+    int m0 = 0;
+    int sel[wbq::kM0Max];
+    for (int t = 0; t < d.ntasks; ++t) {
+        if (d.row_mask[t] <= 0 || d.row_mask[t] >= 64) return WBQ_E_INVALID;
+        for (int r = 0; r < 6; ++r)
+            if ((d.row_mask[t] >> r) & 1) {
+                if (m0 == wbq::kM0Max) return WBQ_E_UNSUPPORTED;
+                sel[m0++] = t * 6 + r;
+            }
+    }
+    wbq_ctx *c = new wbq_ctx();
+    c->d = d;
+    c->d.Kc = c->d.Dc = c->d.Kq = c->d.Dq = c->d.tau_max = c->d.tau_min = nullptr;
+    if (c->d.max_iter <= 0) c->d.max_iter = 4 * d.n + 32;
+    c->m0 = m0;
+    c->device = device;
+    auto cleanup = [&](int rc) {
+        wbq_destroy(c);
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(WBQ_E_DEVICE);
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(WBQ_E_DEVICE);
+    c->stream = c->own_stream;
+    const size_t n = (size_t)d.n, T6 = (size_t)d.ntasks * 6, B = (size_t)d.max_batch;
+    bool ok = hipMalloc(&c->Kc, T6 * 8) == hipSuccess && hipMalloc(&c->Dc, T6 * 8) == hipSuccess &&
+              hipMalloc(&c->Kq, n * 8) == hipSuccess && hipMalloc(&c->Dq, n * 8) == hipSuccess &&
+              hipMalloc(&c->tmax, n * 8) == hipSuccess && hipMalloc(&c->tmin, n * 8) == hipSuccess &&
+              hipMalloc(&c->row_sel, sizeof(int) * wbq::kM0Max) == hipSuccess;
+    for (int f = 0; ok && f < 8; ++f) ok = hipMalloc(&c->own[f], field_elems(d, f) * B * 8) == hipSuccess;
+    ok = ok && hipMalloc(&c->tau, n * B * 8) == hipSuccess && hipMalloc(&c->status, B * 4) == hipSuccess &&
+         hipMalloc(&c->iters, B * 4) == hipSuccess;
+    if (!ok) return cleanup(WBQ_E_DEVICE);
+    ok = hipMemcpy(c->Kc, d.Kc, T6 * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->Dc, d.Dc, T6 * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->Kq, d.Kq, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->Dq, d.Dq, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->tmax, d.tau_max, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->tmin, d.tau_min, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->row_sel, sel, sizeof(int) * m0, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) return cleanup(WBQ_E_DEVICE);
+    *out = c;
+    return WBQ_SUCCESS;
+}
+
+int wbq_set_stream(wbq_ctx *c, void *hip_stream)
+{
+    if (!c) return WBQ_E_INVALID;
+    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+    return WBQ_SUCCESS;
+}
+
+int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
+{
+    if (!c || !in) return WBQ_E_INVALID;
+    if (in->batch < 0 || in->batch > c->d.max_batch)
+        return fail(c, WBQ_E_CAPACITY, "batch exceeds max_batch");
+    const double *src[8] = {in->M, in->J, in->pose, in->pose_ref, in->q, in->qd, in->qref, in->h};
+    for (int f = 0; f < 8; ++f)
+        if (!src[f] && in->batch > 0) return fail(c, WBQ_E_INVALID, "null input pointer");
+    WBQ_HIP(hipSetDevice(c->device));
+    for (int f = 0; f < 8; ++f) {
+        if (in->memory == WBQ_MEM_DEVICE) {
+            c->in[f] = src[f];
+        } else if (in->memory == WBQ_MEM_HOST) {
+            if (in->batch > 0)
+                WBQ_HIP(hipMemcpyAsync(c->own[f], src[f], field_elems(c->d, f) * in->batch * 8,
+                                       hipMemcpyHostToDevice, c->stream));
+            c->in[f] = c->own[f];
+        } else {
+            return fail(c, WBQ_E_INVALID, "unknown memory kind");
+        }
+    }
+    c->batch = in->batch;
+    c->have_inputs = true;
+    return WBQ_SUCCESS;
+}
+
+int wbq_solve(wbq_ctx *c)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "wbq_set_inputs not called");
+    wbq::QppvmArgs a{};
+    a.B = c->batch;
+    a.n = c->d.n;
+    a.ntasks = c->d.ntasks;
+    a.m0 = c->m0;
+    a.select_mode = c->d.select_mode;
+    a.max_iter = c->d.max_iter;
+    for (int t = 0; t < wbq::kTMax; ++t) a.row_mask[t] = t < c->d.ntasks ? c->d.row_mask[t] : 0;
+    a.row_sel = c->row_sel;
+    a.Kc = c->Kc;
+    a.Dc = c->Dc;
+    a.Kq = c->Kq;
+    a.Dq = c->Dq;
+    a.tau_max = c->tmax;
+    a.tau_min = c->tmin;
+    a.M = c->in[0];
+    a.J = c->in[1];
+    a.pose = c->in[2];
+    a.pose_ref = c->in[3];
+    a.q = c->in[4];
+    a.qd = c->in[5];
+    a.qref = c->in[6];
+    a.h = c->in[7];
+    a.tau = c->out_tau ? c->out_tau : c->tau;
+    a.status = c->out_status ? c->out_status : c->status;
+    a.iters = c->out_iters ? c->out_iters : c->iters;
+    WBQ_HIP(hipSetDevice(c->device));
+    const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
+    if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
+    WBQ_HIP(wbq::launch_qppvm(a, c->stream));
+    if (timed) {
+        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+        c->ev_used += 2;
+    }
+    return WBQ_SUCCESS;
+}
+
+int wbq_sync(wbq_ctx *c)
+{
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
+{
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipSetDevice(c->device));
+    const size_t B = (size_t)c->batch;
+    const double *dt = c->out_tau ? c->out_tau : c->tau;
+    const int *ds = c->out_status ? c->out_status : c->status;
+    const int *di = c->out_iters ? c->out_iters : c->iters;
+    if (tau && B) WBQ_HIP(hipMemcpyAsync(tau, dt, B * c->d.n * 8, hipMemcpyDeviceToHost, c->stream));
+    if (status && B) WBQ_HIP(hipMemcpyAsync(status, ds, B * 4, hipMemcpyDeviceToHost, c->stream));
+    if (iters && B) WBQ_HIP(hipMemcpyAsync(iters, di, B * 4, hipMemcpyDeviceToHost, c->stream));
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    return WBQ_SUCCESS;
+}
+
+int wbq_set_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
+{
+    if (!c) return WBQ_E_INVALID;
+    c->out_tau = tau;
+    c->out_status = status;
+    c->out_iters = iters;
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_device_outputs(wbq_ctx *c, const double **tau, const int32_t **status, const int32_t **iters)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (tau) *tau = c->out_tau ? c->out_tau : c->tau;
+    if (status) *status = c->out_status ? c->out_status : c->status;
+    if (iters) *iters = c->out_iters ? c->out_iters : c->iters;
+    return WBQ_SUCCESS;
+}
+
+int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
+{
+    (void)mask;
+    // The dual active set starts cold from the unconstrained optimum every call; there is
+    // no carried working set to drop yet (the solution is unique either way).
+    return c ? WBQ_SUCCESS : WBQ_E_INVALID;
+}
+
+int wbq_set_timing(wbq_ctx *c, int enable)
+{
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipSetDevice(c->device));
+    if (enable && c->ev.empty()) {
+        c->ev.resize(2 * 4096);
+        for (auto &e : c->ev) WBQ_HIP(hipEventCreate(&e));
+    }
+    c->timing = enable != 0;
+    c->ev_used = 0;
+    c->t_acc_ms = 0.0;
+    c->t_launches = 0;
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_timing(wbq_ctx *c, double *total_ms, int *launches)
+{
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipSetDevice(c->device));
+    for (int k = 0; k + 1 < c->ev_used; k += 2) {
+        WBQ_HIP(hipEventSynchronize(c->ev[k + 1]));
+        float ms = 0.f;
+        WBQ_HIP(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
+        c->t_acc_ms += ms;
+        c->t_launches += 1;
+    }
+    c->ev_used = 0;
+    if (total_ms) *total_ms = c->t_acc_ms;
+    if (launches) *launches = c->t_launches;
+    c->t_acc_ms = 0.0;
+    c->t_launches = 0;
+    return WBQ_SUCCESS;
+}
+
+void wbq_destroy(wbq_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    for (auto &e : c->ev) (void)hipEventDestroy(e);
+    double *bufs[] = {c->Kc, c->Dc, c->Kq, c->Dq, c->tmax, c->tmin, c->tau};
+    for (double *p : bufs)
+        if (p) (void)hipFree(p);
+    for (double *p : c->own)
+        if (p) (void)hipFree(p);
+    if (c->row_sel) (void)hipFree(c->row_sel);
+    if (c->status) (void)hipFree(c->status);
+    if (c->iters) (void)hipFree(c->iters);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+}  // extern "C"

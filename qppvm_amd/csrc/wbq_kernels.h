@@ -1,0 +1,36 @@
+// Internal kernel interface of libwbq (not part of the public C ABI, see include/wbq.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace wbq {
+
+constexpr int kWave = 64;
+constexpr int kTMax = 4;    // Cartesian tasks on level 0
+constexpr int kM0Max = 12;  // level-0 rows handled by the kernel
+
+// Everything one launch needs; passed by value as the kernel argument.
+struct QppvmArgs {
+    int B;           // instances
+    int n;           // joints (<= NP of the instantiation)
+    int ntasks;      // Cartesian tasks
+    int m0;          // level-0 rows (selected task rows)
+    int select_mode; // WBQ_SELECT_*
+    int max_iter;    // active-set step cap
+    int row_mask[kTMax];
+    const int *row_sel;      // [m0] task-row index t*6+r of level-0 row a (device)
+    const double *Kc, *Dc;   // [ntasks*6] (device)
+    const double *Kq, *Dq;   // [n]
+    const double *tau_max, *tau_min; // [n]
+    const double *M, *J, *pose, *pose_ref, *q, *qd, *qref, *h;  // batch inputs
+    double *tau;     // [B][n]
+    int *status;     // [B]
+    int *iters;      // [B]
+};
+
+// Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
+hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream);
+
+// Lanes per instance used for a given n (32 for n <= 32, else 64).
+inline int lanes_per_instance(int n) { return n <= 32 ? 32 : 64; }
+
+}  // namespace wbq

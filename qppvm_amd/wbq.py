@@ -1,0 +1,200 @@
+"""ctypes binding of libwbq (include/wbq.h). The product path: HIP kernels on the GPU.
+
+There is no CPU fallback: constructing a solver without the built library or without a
+GPU raises ``WbqError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .problem import INPUT_FIELDS, QPPVMProblem, check_inputs
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwbq.so")
+
+SUCCESS, E_INVALID, E_DEVICE, E_UNSUPPORTED, E_CAPACITY = 0, -1, -2, -3, -4
+MEM_HOST, MEM_DEVICE = 0, 1
+FORM_QPPVM = 0
+
+# every symbol include/wbq.h declares (checked by tests/test_abi.py)
+EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
+           "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
+           "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version")
+
+
+class WbqError(RuntimeError):
+    pass
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("form", ctypes.c_int), ("n", ctypes.c_int), ("ntasks", ctypes.c_int),
+                ("row_mask", ctypes.c_int * 4), ("select_mode", ctypes.c_int),
+                ("joint_weight", ctypes.c_int), ("max_batch", ctypes.c_int),
+                ("max_iter", ctypes.c_int),
+                ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
+                ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+
+
+class Inputs(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int), ("memory", ctypes.c_int)] + \
+               [(k, ctypes.c_void_p) for k in INPUT_FIELDS]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libwbq.so; raises WbqError (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise WbqError(f"{path} not built: run `python -m qppvm_amd.build` (hipcc, gfx950)")
+    lib = ctypes.CDLL(path)
+    P, I = ctypes.c_void_p, ctypes.c_int
+    lib.wbq_create.argtypes = [ctypes.POINTER(Desc), I, ctypes.POINTER(P)]
+    lib.wbq_set_stream.argtypes = [P, P]
+    lib.wbq_set_inputs.argtypes = [P, ctypes.POINTER(Inputs)]
+    lib.wbq_solve.argtypes = [P]
+    lib.wbq_sync.argtypes = [P]
+    lib.wbq_get_outputs.argtypes = [P, P, P, P]
+    lib.wbq_set_outputs.argtypes = [P, P, P, P]
+    lib.wbq_get_device_outputs.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P)]
+    lib.wbq_reset_warmstart.argtypes = [P, P]
+    lib.wbq_set_timing.argtypes = [P, I]
+    lib.wbq_get_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I)]
+    lib.wbq_destroy.argtypes = [P]
+    lib.wbq_destroy.restype = None
+    lib.wbq_last_error.argtypes = [P]
+    lib.wbq_last_error.restype = ctypes.c_char_p
+    lib.wbq_version.restype = ctypes.c_char_p
+    for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
+              "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
+              "wbq_reset_warmstart",
+              "wbq_set_timing", "wbq_get_timing"):
+        getattr(lib, f).restype = I
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class QPPVMSolver:
+    """Batched drop-in for QPPVMPlugin's per-tick solve (tasks + AutoStack + QPOases_sot).
+
+    One context = one device, one HIP stream, buffers sized for ``max_batch``.
+    """
+
+    def __init__(self, prob: QPPVMProblem, max_batch: int, device: int = 0):
+        self.lib = load_library()
+        self.prob = prob
+        self.max_batch = int(max_batch)
+        d = Desc()
+        d.form, d.n, d.ntasks = FORM_QPPVM, prob.n, prob.ntasks
+        for t in range(4):
+            d.row_mask[t] = prob.row_mask[t] if t < prob.ntasks else 0
+        d.select_mode, d.joint_weight = prob.select_mode, prob.joint_weight
+        d.max_batch, d.max_iter = self.max_batch, int(prob.max_iter)
+        self._keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
+                      for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
+        d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [_ptr(a) for a in self._keep]
+        h = ctypes.c_void_p()
+        rc = self.lib.wbq_create(ctypes.byref(d), int(device), ctypes.byref(h))
+        if rc != SUCCESS:
+            raise WbqError(f"wbq_create failed ({rc}): check the GPU / problem support")
+        self.ctx = h
+        self.batch = 0
+        self._host_inputs = None
+
+    # -- errors
+    def _check(self, rc, what):
+        if rc != SUCCESS:
+            msg = self.lib.wbq_last_error(self.ctx).decode()
+            raise WbqError(f"{what} failed ({rc}): {msg}")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.wbq_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- inputs
+    def set_inputs(self, inputs: dict):
+        """Host numpy arrays (copied async H2D into context buffers)."""
+        B = check_inputs(self.prob, inputs)
+        arrs = {k: np.ascontiguousarray(inputs[k], dtype=np.float64) for k in INPUT_FIELDS}
+        self._host_inputs = arrs  # keep alive until the async copy completes
+        s = Inputs(batch=B, memory=MEM_HOST, **{k: _ptr(v) for k, v in arrs.items()})
+        self._check(self.lib.wbq_set_inputs(self.ctx, ctypes.byref(s)), "wbq_set_inputs")
+        self.batch = B
+
+    def set_device_inputs(self, ptrs: dict, batch: int):
+        """Device pointers (e.g. torch tensors' data_ptr()) adopted without copy."""
+        s = Inputs(batch=int(batch), memory=MEM_DEVICE, **{k: int(ptrs[k]) for k in INPUT_FIELDS})
+        self._check(self.lib.wbq_set_inputs(self.ctx, ctypes.byref(s)), "wbq_set_inputs")
+        self.batch = int(batch)
+
+    def set_stream(self, stream_handle: int | None):
+        self._check(self.lib.wbq_set_stream(self.ctx, stream_handle or None), "wbq_set_stream")
+
+    # -- solve
+    def solve(self):
+        self._check(self.lib.wbq_solve(self.ctx), "wbq_solve")
+
+    def sync(self):
+        self._check(self.lib.wbq_sync(self.ctx), "wbq_sync")
+
+    def outputs(self):
+        B, n = self.batch, self.prob.n
+        tau = np.empty((B, n))
+        status = np.empty(B, dtype=np.int32)
+        iters = np.empty(B, dtype=np.int32)
+        self._check(self.lib.wbq_get_outputs(self.ctx, _ptr(tau), _ptr(status), _ptr(iters)),
+                    "wbq_get_outputs")
+        return tau, status, iters
+
+    def set_device_outputs(self, tau_ptr, status_ptr=None, iters_ptr=None):
+        """Write outputs straight into caller-owned device buffers (e.g. torch tensors)."""
+        self._check(self.lib.wbq_set_outputs(self.ctx, tau_ptr or None, status_ptr or None,
+                                             iters_ptr or None), "wbq_set_outputs")
+
+    def device_outputs(self):
+        t, s, i = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self.lib.wbq_get_device_outputs(self.ctx, ctypes.byref(t), ctypes.byref(s),
+                                                    ctypes.byref(i)), "wbq_get_device_outputs")
+        return t.value, s.value, i.value
+
+    def solve_batch(self, inputs: dict):
+        self.set_inputs(inputs)
+        self.solve()
+        return self.outputs()
+
+    def reset_warmstart(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self._check(self.lib.wbq_reset_warmstart(self.ctx, None if m is None else _ptr(m)),
+                    "wbq_reset_warmstart")
+
+    # -- timing (HIP events around every launch, on the launch stream)
+    def set_timing(self, enable: bool):
+        self._check(self.lib.wbq_set_timing(self.ctx, int(bool(enable))), "wbq_set_timing")
+
+    def get_timing(self):
+        ms = ctypes.c_double()
+        cnt = ctypes.c_int()
+        self._check(self.lib.wbq_get_timing(self.ctx, ctypes.byref(ms), ctypes.byref(cnt)),
+                    "wbq_get_timing")
+        return ms.value, cnt.value
+
+
+def version() -> str:
+    return load_library().wbq_version().decode()

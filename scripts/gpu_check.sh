@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, bench, rocprof summary. Every GPU step has its own
+# time limit; a crash / fault / timeout (exit >= 2 from pytest, or any non-zero from the
+# others) ends the script there.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${STEPS:-all}
+run() { # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" ; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  return $rc
+}
+run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ; rc=$?
+if [ $rc -ge 2 ]; then echo "pytest crashed/timed out ($rc): stopping"; exit $rc; fi
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+run bench 300 python bench.py --steps 200 --warmup 20 || exit 1
+if [ "$STEPS" = "all" ]; then
+  run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
+  cd /tmp && run_dir="$GRAFT_REPO_ROOT/gpurun_out/prof"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$run_dir" -o run --output-format csv -- \
+      python "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  echo "prof rc=$?"; tail -n 5 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"
+fi

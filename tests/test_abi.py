@@ -1,0 +1,80 @@
+"""C-ABI checks that need no GPU: the library builds for gfx950, loads, exports every
+symbol include/wbq.h declares, and its struct layouts match the ctypes mirror."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from qppvm_amd import build as wbq_build
+from qppvm_amd import wbq
+
+HEADER = os.path.join(ROOT, "include", "wbq.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\**\s*(wbq_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    wbq_build.build()
+    return wbq.load_library()
+
+
+def test_header_declares_expected_api():
+    assert declared_symbols() == sorted(wbq.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", wbq.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    for name in declared_symbols():
+        assert re.search(rf"\bT {name}$", out, re.M), name
+
+
+def test_code_object_is_gfx950(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", wbq.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr
+
+
+def test_struct_layout_matches_c(tmp_path):
+    prog = tmp_path / "sz.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "wbq.h"\n'
+                    'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(wbq_desc), '
+                    'offsetof(wbq_desc, Kc), sizeof(wbq_inputs), offsetof(wbq_inputs, h));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [ctypes.sizeof(wbq.Desc), wbq.Desc.Kc.offset, ctypes.sizeof(wbq.Inputs),
+                   wbq.Inputs.h.offset]
+
+
+def test_version_string(lib):
+    assert lib.wbq_version().decode().startswith("wbq ")
+
+
+def test_null_arguments_rejected(lib):
+    h = ctypes.c_void_p()
+    assert lib.wbq_create(None, 0, ctypes.byref(h)) == wbq.E_INVALID
+    assert lib.wbq_solve(None) == wbq.E_INVALID
+    assert lib.wbq_sync(None) == wbq.E_INVALID
+    assert lib.wbq_last_error(None) == b"null context"
+    lib.wbq_destroy(None)
+
+
+def test_unsupported_problem_rejected_before_device(lib):
+    d = wbq.Desc()
+    d.form, d.n, d.ntasks, d.max_batch = 7, 30, 2, 4  # unknown form
+    h = ctypes.c_void_p()
+    assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_UNSUPPORTED
+    d.form, d.n = wbq.FORM_QPPVM, 65  # n too large
+    assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_INVALID
