@@ -54,15 +54,19 @@ def main():
     from qppvm_amd.wbq import QPPVMSolver
 
     n, B = args.n, args.batch
+    device = local if dist else 0
     if args.config == 1:
-        prob = QPPVMProblem(n=n, tau_max=1e4)  # bounds inactive
+        prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive
         inp = replicate(qppvm_instances(prob, 1, seed=0), B)
     else:
         inp = qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=rank * B)
-        # ~20 % of the torque bounds active at the solution (calibrated on the unconstrained taus)
-        scale = 1.3 * 10.0 * np.sqrt(n)
-        prob = QPPVMProblem(n=n, tau_max=scale)
-    solver = QPPVMSolver(prob, max_batch=B, device=local if dist else 0)
+        # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the same
+        # batch solved with the limits far away (one extra solve before timing)
+        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B, device=device)
+        tau_free, _, _ = free.solve_batch(inp)
+        free.close()
+        prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
+    solver = QPPVMSolver(prob, max_batch=B, device=device)
     solver.set_inputs(inp)
     solver.sync()
 

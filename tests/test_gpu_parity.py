@@ -60,7 +60,9 @@ def load_b0(prob, inp):
 
 @pytest.mark.parametrize("n", [1, 3, 6, 12, 24, 30, 31, 32, 33, 39, 48, 64])
 def test_random_vs_oracle_bounds_inactive(wbq_mod, oracle_lib, n):
-    prob = QPPVMProblem(n=n, tau_max=1e7, row_mask=(0x7, 0x7) if n >= 6 else (0x1, 0x2))
+    # level 0 stays feasible (m0 <= n): single task with n rows for tiny n
+    kw = dict(ntasks=2, row_mask=(0x7, 0x7)) if n >= 6 else dict(ntasks=1, row_mask=((1 << n) - 1,))
+    prob = QPPVMProblem(n=n, tau_max=1e7, **kw)
     inp = qppvm_instances(prob, 37, seed=100 + n)
     tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
     tau, st, _ = gpu_solve(wbq_mod, prob, inp)
