@@ -23,19 +23,22 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """diag=True builds libwbq_diag.so with in-kernel phase stamps (never the product)."""
+    lib = LIB.replace("libwbq.so", "libwbq_diag.so") if diag else LIB
+    if not force and not diag and not _stale():
         return LIB
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
            "-I", os.path.join(ROOT, "include"),
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+           *(["-DWBQ_STAMPS"] if diag else []),
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

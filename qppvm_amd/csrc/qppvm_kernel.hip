@@ -1,8 +1,17 @@
-// qppvm_kernel.hip -- fused batched QPPVM torque solve for gfx950 (MI355X), fp64.
+// qppvm_kernel.hip -- batched QPPVM torque solve for gfx950 (MI355X), fp64.
 //
 // One QP instance per group of NP lanes (NP = 32: two instances per wave64; NP = 64: one),
-// lane i <-> joint i. A launch covers assemble -> 2-level hierarchical QP -> tau for
-// the whole batch; nothing goes back to the host in between.
+// lane i <-> joint i. A solve is two launches on one stream, nothing goes back to the host:
+//
+//   qppvm_fast_kernel    every instance: stage -> task forces -> Gauss-Jordan on M ->
+//                        equality-constrained optimum -> bound check -> tau. Instances whose
+//                        optimum violates a torque bound park (u, Q1) in scratch and append
+//                        themselves to a device work queue.
+//   qppvm_active_kernel  grid-stride over that queue only: Goldfarb-Idnani dual active set on
+//                        the torque bounds -> tau. Its last block resets the queue.
+//
+// The split keeps the common path lean (VGPRs, LDS, hence occupancy) and gives the iterative
+// part its own resource budget.
 //
 // The math (reference src/QPPVMPlugin.cpp:201-259):
 //   level 0  min 0.5 sum_t ||S_t J_t M^-1 x - S_t J_t M^-1 J_t^T F_t||^2      (:129-152, :177)
@@ -13,21 +22,13 @@
 // least-distance problem
 //   min 0.5 ||u - u_imp||^2  s.t.  G u = b0,  lo <= M u <= hi
 // with G = stacked selected rows of J (given data) and u_imp = M^-1 tau_imp. The Hessian
-// is the identity, so the Goldfarb-Idnani dual active set needs no factorisation of H,
-// the bound normals are rows of M (given data), and the conditioning is cond(M), not
-// cond(M)^2 as in the reference's x-space H1 = M^-2. When level 0 is feasible
-// (y* = b0, the generic case) the level-0 optimality constraint A0 x = y* is exactly
-// G u = b0; an infeasible level 0 is reported as status 2 by this kernel.
+// is the identity, so the dual active set needs no factorisation of H, the bound normals
+// are rows of M (given data), and the conditioning is cond(M), not cond(M)^2 as in the
+// reference's x-space H1 = M^-2. When level 0 is feasible (y* = b0, the generic case) the
+// level-0 optimality constraint A0 x = y* is exactly G u = b0; an infeasible level 0 is
+// reported as status 2.
 //
-// Per instance:
-//   1. stage J rows / poses / q, qd in LDS, task-space force F_t = Kc e - Dc J qd;
-//   2. Gauss-Jordan on [M | tau_imp, J_t^T F_t] in registers (M SPD: no pivoting; the
-//      trailing block stays symmetric, so the pivot row is read back from the pivot
-//      column every lane just published) -> u_imp, w_t = M^-1 J_t^T F_t;
-//   3. b0 = G w, Cholesky-QR of G^T (rank-revealing) -> Q1, u_eq = u_imp + Q1 R^-T (b0 - G u_imp);
-//   4. GI iterations on the bound rows of M: d1 = Q1^T n_p, z = (I - Q1 Q1^T) n_p (twice,
-//      CGS2), r = R_II^-1 d1_I kept through T = R_II^-1, primal/dual steps, add/drop;
-//   5. tau = M u + h.
+// M must be symmetric (it is read column-wise as rows).
 #include "wbq_kernels.h"
 
 #include <math.h>
@@ -37,37 +38,90 @@ namespace {
 
 constexpr double kInf = 1.0e300;
 
-// Per-instance LDS layout in doubles (T = ntasks is a launch constant).
-// Rows of NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
+// Phase stamps for the diagnostic build only (never compiled into the product library).
+#ifdef WBQ_STAMPS
+#define WBQ_STAMP(k)                                                                    \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                     \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (threadIdx.x == 0 && a.stamps) a.stamps[blockIdx.x * kStamps + (k)] = t_;    \
+    } while (0)
+#else
+#define WBQ_STAMP(k) do {} while (0)
+#endif
+
+
+// Per-instance LDS layouts in doubles (T = ntasks and m0 are launch constants). Rows of
+// NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
 template <int NP>
-struct Layout {
-    static constexpr bool MREG = (NP == 32); // M rows in VGPRs (else in LDS)
-    static constexpr int RS = NP + 1;        // row stride
-    int MA, QA, TT, JR, BC, RH, U, D1, D1B, NV, WV, QD, F, B0, RES, RHO, GR, LC, PS, SIZE;
-    __host__ __device__ Layout(int T)
+struct FastLayout {
+    int JR, BC, RH, U, WV, QD, F, B0, RES, RHO, CV, GR, ID, LC, PS, SIZE;
+    __host__ __device__ FastLayout(int T, int m0)
     {
-        MA = 0;                                     // staged M rows
-        QA = MREG ? MA : MA + NP * RS;              // Q1^T rows (reuses MA once M is in VGPRs)
-        TT = QA + NP * RS;                          // T = R_II^-1 rows (NP == 64 only)
-        JR = TT + (NP == 64 ? NP * RS : 0);         // J rows [T*6][NP]
-        BC = JR + T * 6 * NP;                       // GJ pivot column, double-buffered [2][NP]
-        RH = BC + 2 * NP;                           // GJ pivot right-hand sides [2][8]
-        U = RH + 16;                                // u
-        D1 = U + NP;                                // d1 = Q1^T n_p, zero-padded to 2 NP
-        D1B = D1 + 2 * NP;                          // second Gram-Schmidt pass
-        NV = D1B + NP;                              // n_p
-        WV = NV + NP;                               // w_t [T][NP]
-        QD = WV + T * NP;                           // qdot
-        F = QD + NP;                                // task forces [T*6]
-        B0 = F + 6 * T;                             // b0 [kM0Max]
-        RES = B0 + kM0Max;                          // b0 - G u_imp
-        RHO = RES + kM0Max;                         // L^-1 (b0 - G u_imp)
-        GR = RHO + kM0Max;                          // Gram, then its Cholesky factor L
-        LC = GR + kM0Max * kM0Max;                  // broadcast column of L
-        PS = LC + kM0Max;                           // poses [T][24]
-        SIZE = (PS + 24 * T + 1) & ~1;              // keep 16-B alignment of the next instance
+        JR = 0;                  // J rows [T*6][NP]
+        BC = JR + T * 6 * NP;    // GJ pivot column, double-buffered [2][NP]
+        RH = BC + 2 * NP;        // GJ pivot right-hand sides [2][8]
+        U = RH + 16;             // u
+        WV = U + NP;             // w_t [T][NP]
+        QD = WV + T * NP;        // qdot
+        F = QD + NP;             // task forces [T*6]
+        B0 = F + 6 * T;          // b0 [m0]
+        RES = B0 + m0;           // b0 - G u_imp
+        RHO = RES + m0;          // L^-1 (b0 - G u_imp)
+        CV = RHO + m0;           // L^-T rho
+        GR = CV + m0;            // Gram, then its Cholesky factor L [m0][kM0Max]
+        ID = GR + m0 * kM0Max;   // 1 / L_cc (0 for dependent rows)
+        LC = ID + kM0Max;        // broadcast column of L
+        PS = LC + kM0Max;        // poses [T][24]
+        SIZE = (PS + 24 * T + 1) & ~1;
     }
 };
+
+template <int NP>
+struct ActiveLayout {
+    static constexpr bool MREG = (NP == 32); // M rows and T rows in VGPRs (else in LDS)
+    static constexpr int RS = NP + 1;
+    int QA, MA, TT, U, D1, D1B, NV, BC, SIZE;
+    __host__ __device__ ActiveLayout(int, int)
+    {
+        QA = 0;                           // Q1^T rows [NP][RS]
+        MA = QA + NP * RS;                // M rows (NP == 64)
+        TT = MA + (MREG ? 0 : NP * RS);   // T = R_II^-1 rows (NP == 64)
+        U = TT + (MREG ? 0 : NP * RS);    // u
+        D1 = U + NP;                      // d1 = Q1^T n_p, zero-padded to 2 NP
+        D1B = D1 + 2 * NP;                // second Gram-Schmidt pass
+        NV = D1B + NP;                    // n_p
+        BC = NV + NP;                     // broadcast scratch
+        SIZE = (BC + NP + 1) & ~1;
+    }
+};
+
+// fast reciprocal / reciprocal square root: hardware estimate + one Newton step (~0.5 ulp)
+__device__ __forceinline__ double frcp(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double frsq(double x)
+{
+    double y = __builtin_amdgcn_rsq(x);
+    return y * fma(-0.5 * x * y, y, 1.5);
+}
+
+// Raw buffer loads: one 32-bit per-lane byte offset + a uniform SGPR offset per load, so an
+// unrolled run of loads costs no address VGPRs (a flat load would need a 64-bit address each).
+// Out-of-range offsets read 0 (hardware bounds check on num_records).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double *p, long elems)
+{
+    const long bytes = elems * 8;
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                             0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff_bytes, soff_bytes, 0));
+}
 
 // One row of an NP-column matrix per lane: in VGPRs (compile-time indices, runtime
 // writes by select) or in LDS.
@@ -210,18 +264,12 @@ __device__ double cart_error_component(const double *P, const double *Pr, int r)
     return sg * (r == 3 ? qx : (r == 4 ? qy : qz));
 }
 
-template <int NP>
-__device__ __forceinline__ void load_row(RowStore<NP, true> &R, const double *Mb, int n, int i, bool row)
-{
-#pragma unroll
-    for (int j = 0; j < NP; ++j) R.v[j] = (row && j < n) ? Mb[i * n + j] : (j == i ? 1.0 : 0.0);
-}
 
 // Orthogonalise the normal held in NV against the rows of Q1T (two classical Gram-Schmidt
 // passes). Rows >= q of Q1T are finite and D1[c >= q] = 0, so every loop runs to NP
 // unguarded. Leaves d1 = Q1^T n in D1 and returns this lane's entry of z.
 template <int NP>
-__device__ __forceinline__ double project_out(double *S, const Layout<NP> &L, double npj, int q, int i)
+__device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> &L, double npj, int q, int i)
 {
     constexpr int RS = NP + 1;
     double d1 = 0.0;
@@ -250,15 +298,15 @@ __device__ __forceinline__ double project_out(double *S, const Layout<NP> &L, do
     return z;
 }
 
+
+// ====================================================================== fast path
 template <int NP>
-__global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
+__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
-    constexpr int RS = NP + 1;
-    constexpr bool MREG = Layout<NP>::MREG;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int T = a.ntasks, n = a.n, m0 = a.m0;
-    const Layout<NP> L(T);
+    const FastLayout<NP> L(T, m0);
     const int tid = threadIdx.x;
     const int sub = tid / NP;
     const int i = tid - sub * NP;
@@ -267,30 +315,50 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
     double *S = smem + sub * L.SIZE;
     const bool row = valid && i < n;
     const long bn = valid ? b * n : 0;
+    const int ic = i < n ? i : n - 1; // clamped column for unconditional loads
+    WBQ_STAMP(0);
 
     // ---------------------------------------------------------------- 1. stage
-    const double q_i = row ? a.q[bn + i] : 0.0;
-    const double qd_i = row ? a.qd[bn + i] : 0.0;
-    const double qref_i = row ? a.qref[bn + i] : 0.0;
-    const double h_i = row ? a.h[bn + i] : 0.0;
-    S[L.QD + i] = qd_i;
-    const double *Mb = a.M + (valid ? b * n * n : 0);
-    {
-        // M row by row: every load instruction reads whole contiguous rows (coalesced)
+    // Every global load is unconditional (clamped offsets, values selected afterwards), so
+    // they issue back to back: one HBM round trip.
+    const long Bn = (long)a.B * n;
+    const int voff = (int)(8 * (bn + ic));
+    const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
+    const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
+    const int moff = (int)(8 * ((valid ? b * n * n : 0) + ic));
+    // M is symmetric: lane i's row is its column, so row r of M read across lanes is
+    // contiguous -- coalesced loads straight into the elimination registers.
+    double A[NP];
 #pragma unroll
-        for (int r = 0; r < NP; ++r)
-            if (r < n) S[L.MA + r * RS + i] = row ? Mb[r * n + i] : 0.0;
-        const double *Jb = a.J + (valid ? b * T * 6 * n : 0);
-        for (int rr = 0; rr < T * 6; ++rr) S[L.JR + rr * NP + i] = row ? Jb[rr * n + i] : 0.0;
-        for (int e = i; e < T * 24; e += NP) {
-            const int t = e / 24, c = e - t * 24;
-            double v = 0.0;
-            if (valid)
-                v = (c < 12) ? a.pose[(b * T + t) * 12 + c] : a.pose_ref[(b * T + t) * 12 + c - 12];
-            S[L.PS + e] = v;
-        }
-        S[L.D1 + NP + i] = 0.0; // zero pad of d1
+    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    double jv[kTMax * 6];
+    {
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.J, Bn * T * 6);
+        const int joff = (int)(8 * ((valid ? b * T * 6 * n : 0) + ic));
+#pragma unroll
+        for (int rr = 0; rr < kTMax * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
     }
+    constexpr int kPoseIt = (kTMax * 24 + NP - 1) / NP;
+    double pv[kPoseIt];
+#pragma unroll
+    for (int it = 0; it < kPoseIt; ++it) {
+        int e = it * NP + i;
+        e = e < T * 24 ? e : T * 24 - 1;
+        const int t = e / 24, c = e - t * 24;
+        const long base = valid ? b * T * 12 : 0;
+        pv[it] = (c < 12) ? a.pose[base + t * 12 + c] : a.pose_ref[base + t * 12 + c - 12];
+    }
+    const double h_i = row ? h_i0 : 0.0;
+    S[L.QD + i] = row ? qd_i : 0.0;
+#pragma unroll
+    for (int rr = 0; rr < kTMax * 6; ++rr)
+        if (rr < T * 6) S[L.JR + rr * NP + i] = row ? jv[rr] : 0.0;
+#pragma unroll
+    for (int it = 0; it < kPoseIt; ++it)
+        if (it * NP + i < T * 24) S[L.PS + it * NP + i] = valid ? pv[it] : 0.0;
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     __syncthreads();
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
@@ -303,25 +371,12 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
         S[L.F + i] = F;
     }
-    // rows of M into VGPRs (A for the elimination, Mr kept for the bound rows)
-    double A[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) A[j] = (row && j < n) ? S[L.MA + i * RS + j] : (j == i ? 1.0 : 0.0);
-    RowStore<NP, MREG> Mr;
-    Mr.bind(S + L.MA + i * RS);
-    if constexpr (MREG) {
-#pragma unroll
-        for (int j = 0; j < NP; ++j) Mr.v[j] = A[j];
-    } else {
-        // pad rows/columns of the LDS copy as identity
-        for (int j = 0; j < NP; ++j)
-            if (!(row && j < n)) S[L.MA + i * RS + j] = (j == i ? 1.0 : 0.0);
-    }
     __syncthreads();
+    WBQ_STAMP(1);
 
     // ------------------------------------------------- 2. Gauss-Jordan, M SPD
     double rhs[1 + kTMax];
-    rhs[0] = row ? a.Kq[i] * (qref_i - q_i) - a.Dq[i] * qd_i : 0.0; // tau_imp (:105-106)
+    rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
 #pragma unroll
     for (int t = 0; t < kTMax; ++t) {
         double c = 0.0;
@@ -332,35 +387,52 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
     }
     double dval = 1.0;
     bool notspd = false;
+    // M SPD: no pivoting, and the trailing block stays symmetric, so the pivot row is the
+    // pivot column every lane publishes. Step k reads buffer k&1 and publishes column k+1
+    // into the other buffer as soon as it is updated (lookahead).
+    S[L.BC + i] = A[0];
+    if (i == 0) {
+#pragma unroll
+        for (int m = 0; m < 1 + kTMax; ++m) S[L.RH + m] = rhs[m];
+    }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         if (k < n) {
-            double *bc = S + L.BC + (k & 1) * NP;
-            double *rh = S + L.RH + (k & 1) * 8;
-            bc[i] = A[k];
-            if (i == k) {
-#pragma unroll
-                for (int m = 0; m < 1 + kTMax; ++m) rh[m] = rhs[m];
-            }
             __syncthreads();
+            const double *bc = S + L.BC + (k & 1) * NP;
+            const double *rh = S + L.RH + (k & 1) * 8;
+            double *bcn = S + L.BC + ((k + 1) & 1) * NP;
+            double *rhn = S + L.RH + ((k + 1) & 1) * 8;
             const double piv = bc[k];
             notspd |= !(piv > 0.0);
-            const double f = (i == k) ? 0.0 : A[k] / piv;
-#pragma unroll
-            for (int j = k + 1; j < NP; ++j) A[j] = fma(-f, bc[j], A[j]);
+            const double f = (i == k) ? 0.0 : A[k] * frcp(piv);
 #pragma unroll
             for (int m = 0; m < 1 + kTMax; ++m) rhs[m] = fma(-f, rh[m], rhs[m]);
+            if (k + 1 < NP) {
+                A[k + 1] = fma(-f, bc[k + 1], A[k + 1]);
+                if (k + 1 < n) {
+                    bcn[i] = A[k + 1];
+                    if (i == k + 1) {
+#pragma unroll
+                        for (int m = 0; m < 1 + kTMax; ++m) rhn[m] = rhs[m];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = k + 2; j < NP; ++j) A[j] = fma(-f, bc[j], A[j]);
             dval = (i == k) ? piv : dval;
         }
     }
-    const double u_imp = rhs[0] / dval;
+    const double dinv = frcp(dval);
+    const double u_imp = rhs[0] * dinv;
     S[L.U + i] = u_imp;
 #pragma unroll
     for (int t = 0; t < kTMax; ++t)
-        if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] / dval; // w_t = M^-1 J_t^T F_t
+        if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] * dinv; // w_t = M^-1 J_t^T F_t
     __syncthreads();
+    WBQ_STAMP(2);
 
-    // ---------------------------------- 3. level-0 rows and the equality block
+    // ------------------------------ 3. level-0 rows: G u = b0 in least distance from u_imp
     if (i < m0) {
         const int rr = a.row_sel[i], t = rr / 6;
         double bb = 0.0, gu = 0.0;
@@ -370,14 +442,16 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
             bb = fma(g, S[L.WV + t * NP + j], bb);
             gu = fma(g, S[L.U + j], gu);
         }
-        S[L.B0 + i] = bb;           // b0 = S J M^-1 J^T F
+        S[L.B0 + i] = bb;          // b0 = S J M^-1 J^T F
         S[L.RES + i] = bb - gu;
     }
     {
+        // Gram G G^T, lower triangle: one (row, col) pair per lane
         const int npairs = m0 * (m0 + 1) / 2;
         for (int pp = i; pp < npairs; pp += NP) {
-            int ra = 0;
-            while ((ra + 1) * (ra + 2) / 2 <= pp) ++ra;
+            int ra = (int)((sqrtf(8.0f * pp + 1.0f) - 1.0f) * 0.5f);
+            ra += ((ra + 1) * (ra + 2) / 2 <= pp) ? 1 : 0;
+            ra -= (ra * (ra + 1) / 2 > pp) ? 1 : 0;
             const int ca = pp - ra * (ra + 1) / 2;
             const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
             double g = 0.0;
@@ -401,18 +475,19 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
 #pragma unroll
         for (int c = 0; c < kM0Max; ++c) gdiag = (c == i) ? g[c] : gdiag;
         const double dmx = imax<NP>(gdiag);
-        __syncthreads();
 #pragma unroll
         for (int c = 0; c < kM0Max; ++c) {
             if (c < m0) {
                 const double dc = __shfl(g[c], c, NP);
                 const bool indep = dc > 1e-12 * dmx;
-                const double Lcc = indep ? sqrt(dc) : 0.0;
-                const double lrc = (i > c && indep) ? g[c] / Lcc : (i == c ? Lcc : 0.0);
-                const double rc = __shfl(res, c, NP);
-                const double rho_c = indep ? rc / Lcc : 0.0;
+                const double il = indep ? frsq(dc) : 0.0; // 1 / L_cc
+                const double lrc = (i > c) ? g[c] * il : (i == c ? dc * il : 0.0);
+                const double rho_c = __shfl(res, c, NP) * il;
                 if (i > c) res = fma(-lrc, rho_c, res);
-                if (i == c) S[L.RHO + c] = rho_c;
+                if (i == c) {
+                    S[L.RHO + c] = rho_c;
+                    S[L.ID + c] = il;
+                }
                 if (i < m0) {
                     S[L.LC + i] = lrc;
                     S[L.GR + i * kM0Max + c] = lrc;
@@ -420,26 +495,28 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
                 __syncthreads();
 #pragma unroll
                 for (int j = c + 1; j < kM0Max; ++j) g[j] = fma(-lrc, S[L.LC + j], g[j]);
-                __syncthreads();
             }
         }
     }
-    // Q1 = G^T L^-T (row i of Q1 by forward substitution), u_eq = u_imp + Q1 rho
-    double q1[kM0Max];
-    double u_i = u_imp;
+    __syncthreads();
+    // c = L^-T rho (every lane, from LDS broadcasts), u_eq = u_imp + G^T c
+    double cv[kM0Max];
 #pragma unroll
-    for (int c = 0; c < kM0Max; ++c) {
+    for (int c = kM0Max - 1; c >= 0; --c) {
         double v = 0.0;
         if (c < m0) {
-            v = S[L.JR + a.row_sel[c] * NP + i];
+            v = S[L.RHO + c];
 #pragma unroll
-            for (int k = 0; k < c; ++k) v = fma(-S[L.GR + c * kM0Max + k], q1[k], v);
-            const double d = S[L.GR + c * kM0Max + c];
-            v = d > 0.0 ? v / d : 0.0;
-            u_i = fma(v, S[L.RHO + c], u_i);
+            for (int k = c + 1; k < kM0Max; ++k)
+                if (k < m0) v = fma(-S[L.GR + k * kM0Max + c], cv[k], v);
+            v *= S[L.ID + c];
         }
-        q1[c] = v;
+        cv[c] = v;
     }
+    double u_i = u_imp;
+#pragma unroll
+    for (int c = 0; c < kM0Max; ++c)
+        if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
     S[L.U + i] = u_i;
     __syncthreads();
     // residual of every level-0 row (catches rows dropped as dependent: level 0 infeasible)
@@ -453,183 +530,297 @@ __global__ __launch_bounds__(64) void qppvm_solve_kernel(const QppvmArgs a)
         eqres = fabs(gu - bb) / fmax(1.0, fabs(bb));
     }
     eqres = imax<NP>(eqres);
-    // Q1^T rows: the m0 equality directions, zero beyond
-#pragma unroll
-    for (int c = 0; c < NP; ++c) S[L.QA + c * RS + i] = (c < kM0Max && c < m0) ? q1[c < kM0Max ? c : 0] : 0.0;
-    __syncthreads();
+    WBQ_STAMP(3);
 
-    // ------------------------------ 4. Goldfarb-Idnani on the torque bounds
-    double nrm2 = 0.0;
+    // ------------------------------------------------------------ 4. bound check
+    // x = M u with M's rows re-read (coalesced, L2-hot) into the registers A freed
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const double mij = Mr.get(j);
-        nrm2 = fma(mij, mij, nrm2);
-    }
-    const double nrm = sqrt(nrm2);
-    const double lo = row ? a.tau_min[i] - h_i : -kInf;
-    const double hi = row ? a.tau_max[i] - h_i : kInf;
-    RowStore<NP, NP == 32> Tr;
-    Tr.bind(S + L.TT + i * RS);
-    Tr.zero();
-
+    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    double x_i = 0.0;
+#pragma unroll
+    for (int r = 0; r < NP; ++r) x_i = fma((row && r < n) ? A[r] : (r == i ? 1.0 : 0.0), S[L.U + r], x_i);
+    const double lo = row ? a.tau_min[ic] - h_i : -kInf;
+    const double hi = row ? a.tau_max[ic] - h_i : kInf;
     int status = 0;
     if (imax<NP>((row && lo > hi) ? 1.0 : 0.0) > 0.0) status = 2; // crossed limits
-    if (notspd) status = 3;
-    if (status == 0 && eqres > 1e-9) status = 2; // level 0 infeasible (not handled here)
-    bool go = valid && status == 0;
-    int k = 0, q = m0, iters = 0;
-    int act_p = -1, act_s = 0; // lane a < k: active inequality a (row index, sign)
-    double lam = 0.0;          // lane a < k: its multiplier
-    int p = 0, sg = 1;
-    double lamp = 0.0;
-    bool need_select = true;
-    const int maxit = a.max_iter;
+    if (imax<NP>(notspd ? 1.0 : 0.0) > 0.0) status = 3;
+    if (status == 0 && eqres > 1e-9) status = 2; // level 0 infeasible
+    double viol = 0.0;
+    if (row) {
+        const double tol = 1e-10 * fmax(1.0, fmax(fabs(x_i), fmax(fabs(lo), fabs(hi))));
+        if (fmax(lo - x_i, x_i - hi) > tol) viol = 1.0;
+    }
+    const bool active = imax<NP>(viol) > 0.0 && status == 0 && valid;
+    if (!active) {
+        double tau_i = x_i + h_i;
+        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+        if (row) a.tau[bn + i] = tau_i;
+        if (valid && i == 0) {
+            a.status[b] = status;
+            a.iters[b] = 0;
+        }
+    } else {
+        // park (u, Q1) for the active-set kernel; Q1 = G^T L^-T row by row
+        double q1[kM0Max];
+#pragma unroll
+        for (int c = 0; c < kM0Max; ++c) {
+            double v = 0.0;
+            if (c < m0) {
+                v = S[L.JR + a.row_sel[c] * NP + i];
+#pragma unroll
+                for (int k = 0; k < c; ++k) v = fma(-S[L.GR + c * kM0Max + k], q1[k], v);
+                v *= S[L.ID + c];
+            }
+            q1[c] = v;
+        }
+        double *us = a.u_scr + b * NP;
+        double *qs = a.q1_scr + b * kM0Max * NP;
+        us[i] = u_i;
+#pragma unroll
+        for (int c = 0; c < kM0Max; ++c)
+            if (c < m0) qs[c * NP + i] = q1[c];
+        if (i == 0) a.queue[atomicAdd(a.qcount, 1)] = (int)b;
+    }
+    WBQ_STAMP(5);
+}
 
-    while (__any(go)) {
-        const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
-        if (need_select) {
-            double v = -1.0;
-            if (row) {
-                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
-                const double viol = fmax(lo - s_i, s_i - hi);
-                if (viol > tol) v = viol / nrm;
-            }
-            int pi = i;
-            iargmax<NP>(v, pi);
-            if (!(v > 0.0)) go = false; // optimal
-            p = pi;
-            sg = (__shfl(lo - s_i, p, NP) > __shfl(s_i - hi, p, NP)) ? 1 : -1;
-            lamp = 0.0;
+// ============================================================== active-set path
+template <int NP>
+__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
+{
+    constexpr int IPW = kWave / NP;
+    constexpr int RS = NP + 1;
+    constexpr bool MREG = ActiveLayout<NP>::MREG;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int n = a.n, m0 = a.m0;
+    const ActiveLayout<NP> L(a.ntasks, m0);
+    const int tid = threadIdx.x;
+    const int sub = tid / NP;
+    const int i = tid - sub * NP;
+    double *S = smem + sub * L.SIZE;
+    const int count = __hip_atomic_load(a.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long Bn = (long)a.B * n;
+    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
+    const int ic = i < n ? i : n - 1;
+
+    for (int base = blockIdx.x * IPW; base < count; base += gridDim.x * IPW) {
+        const int e = base + sub;
+        const bool valid = e < count;
+        const long b = valid ? a.queue[e] : 0;
+        const bool row = valid && i < n;
+        const long bn = b * n;
+        const int moff = (int)(8 * (b * n * n + ic));
+        // M rows (columns, coalesced), h, limits, u and Q1 from the fast kernel
+        RowStore<NP, MREG> Mr;
+        Mr.bind(S + L.MA + i * RS);
+        double mrow[NP];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+#pragma unroll
+        for (int r = 0; r < NP; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
+        if constexpr (MREG) {
+#pragma unroll
+            for (int r = 0; r < NP; ++r) Mr.v[r] = mrow[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < NP; ++r) S[L.MA + i * RS + r] = mrow[r];
         }
-        const double s_p = __shfl(s_i, p, NP);
-        const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
-        const double npn = __shfl(nrm, p, NP);
-        const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
-        S[L.NV + i] = npj;
+        const double h_i = row ? a.h[bn + i] : 0.0;
+        const double lo = row ? a.tau_min[i] - h_i : -kInf;
+        const double hi = row ? a.tau_max[i] - h_i : kInf;
+        double u_i = valid ? a.u_scr[b * NP + i] : 0.0;
+        const double *qs = a.q1_scr + b * kM0Max * NP;
+#pragma unroll
+        for (int c = 0; c < NP; ++c)
+            S[L.QA + c * RS + i] = (valid && c < kM0Max && c < m0) ? qs[(c < kM0Max ? c : 0) * NP + i] : 0.0;
+        S[L.D1 + NP + i] = 0.0;
+        S[L.U + i] = u_i;
+        RowStore<NP, MREG> Tr;
+        Tr.bind(S + L.TT + i * RS);
+        Tr.zero();
+        double nrm2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) nrm2 = fma(mrow[j], mrow[j], nrm2);
+        const double nrm = sqrt(nrm2);
         __syncthreads();
-        const double z = project_out<NP>(S, L, npj, q, i);
-        const double zz = isum<NP>(z * z);
-        double ra = 0.0;
-        if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
-        const double rmax = imax<NP>(fabs(ra));
-        double cand = (i < k && ra > 1e-13 * rmax) ? lam / ra : kInf;
-        int ci = i;
-        iargmin<NP>(cand, ci);
-        const double t1 = cand;
-        const double t2 = (zz > 1e-20 * npn * npn) ? -sp / zz : kInf;
-        bool rebuild = false;
-        int cdrop = 0;
-        if (go && t1 >= kInf && t2 >= kInf) {
-            status = 2; // infeasible
-            go = false;
-        }
-        if (go) {
-            const double t = fmin(t1, t2);
-            if (i < k) lam = fma(-t, ra, lam);
-            lamp += t;
-            if (t2 < kInf) u_i = fma(t, z, u_i);
-            ++iters;
-            if (t2 <= t1) { // add p
-                const double iz = 1.0 / sqrt(zz);
-                S[L.QA + q * RS + i] = z * iz;
-                if (i < k) Tr.set(k, -ra * iz);
-                if (i == k) {
-                    Tr.zero();
-                    Tr.set(k, iz);
-                    act_p = p;
-                    act_s = sg;
-                    lam = lamp;
+
+        int status = 0;
+        bool go = valid;
+        int k = 0, q = m0, iters = 0;
+        int act_p = -1, act_s = 0; // lane a < k: active inequality a (row index, sign)
+        double lam = 0.0;          // lane a < k: its multiplier
+        int p = 0, sg = 1;
+        double lamp = 0.0;
+        bool need_select = true;
+        const int maxit = a.max_iter;
+
+        while (true) {
+            const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
+            if (need_select) {
+                double v = -1.0;
+                if (row) {
+                    const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                    const double viol = fmax(lo - s_i, s_i - hi);
+                    if (viol > tol) v = viol / nrm;
                 }
-                ++k;
-                ++q;
-                need_select = true;
-            } else { // drop ci (its multiplier hit zero), keep p
-                const int nap = __shfl(act_p, i + 1, NP);
-                const int nas = __shfl(act_s, i + 1, NP);
-                const double nlam = __shfl(lam, i + 1, NP);
-                if (i >= ci) {
-                    act_p = nap;
-                    act_s = nas;
-                    lam = nlam;
-                }
-                --k;
-                cdrop = ci;
-                q = m0 + ci;
-                rebuild = true;
-                need_select = false;
+                int pi = i;
+                iargmax<NP>(v, pi);
+                if (!(v > 0.0)) go = false; // optimal
+                p = pi;
+                sg = (__shfl(lo - s_i, p, NP) > __shfl(s_i - hi, p, NP)) ? 1 : -1;
+                lamp = 0.0;
             }
-            if (iters >= maxit && go) {
-                status = 1;
+            if (!__any(go)) break;
+            const double s_p = __shfl(s_i, p, NP);
+            const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
+            const double npn = __shfl(nrm, p, NP);
+            const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
+            S[L.NV + i] = npj;
+            __syncthreads();
+            const double z = project_out<NP>(S, L, npj, q, i);
+            const double zz = isum<NP>(z * z);
+            double ra = 0.0;
+            if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
+            const double rmax = imax<NP>(fabs(ra));
+            double cand = (i < k && ra > 1e-13 * rmax) ? lam / ra : kInf;
+            int ci = i;
+            iargmin<NP>(cand, ci);
+            const double t1 = cand;
+            const double t2 = (zz > 1e-20 * npn * npn) ? -sp / zz : kInf;
+            bool rebuild = false;
+            int cdrop = 0;
+            if (go && t1 >= kInf && t2 >= kInf) {
+                status = 2; // infeasible
                 go = false;
             }
-        }
-        S[L.U + i] = u_i;
-        __syncthreads();
-        if (__any(rebuild)) {
-            // Re-factor the inequality directions from the dropped position on: Q1T rows
-            // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
-            if (rebuild && i < NP) {
-#pragma unroll
-                for (int j = 0; j < NP; ++j)
-                    if (j >= cdrop) Tr.set(j, 0.0);
-            }
-            const int kk = rebuild ? k : 0;
-            int kmax = kk, amin = rebuild ? cdrop : NP;
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                kmax = max(kmax, __shfl_xor(kmax, m, 64));
-                amin = min(amin, __shfl_xor(amin, m, 64));
-            }
-            for (int a2 = amin; a2 < kmax; ++a2) {
-                const bool on = rebuild && a2 >= cdrop && a2 < kk;
-                const int pa = __shfl(act_p, a2, NP), sa = __shfl(act_s, a2, NP);
-                const double nj = on ? sa * Mr.get(pa) : 0.0;
-                S[L.NV + i] = nj;
-                __syncthreads();
-                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
-                const double zzr = isum<NP>(zr * zr);
-                double rr2 = 0.0;
-                if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
-                if (on) {
-                    const double iz = 1.0 / sqrt(zzr);
-                    S[L.QA + q * RS + i] = zr * iz;
-                    if (i < a2) Tr.set(a2, -rr2 * iz);
-                    if (i == a2) Tr.set(a2, iz);
+            if (go) {
+                const double t = fmin(t1, t2);
+                if (i < k) lam = fma(-t, ra, lam);
+                lamp += t;
+                if (t2 < kInf) u_i = fma(t, z, u_i);
+                ++iters;
+                if (t2 <= t1) { // add p
+                    const double iz = frsq(zz);
+                    S[L.QA + q * RS + i] = z * iz;
+                    if (i < k) Tr.set(k, -ra * iz);
+                    if (i == k) {
+                        Tr.zero();
+                        Tr.set(k, iz);
+                        act_p = p;
+                        act_s = sg;
+                        lam = lamp;
+                    }
+                    ++k;
                     ++q;
+                    need_select = true;
+                } else { // drop ci (its multiplier hit zero), keep p
+                    const int nap = __shfl(act_p, i + 1, NP);
+                    const int nas = __shfl(act_s, i + 1, NP);
+                    const double nlam = __shfl(lam, i + 1, NP);
+                    if (i >= ci) {
+                        act_p = nap;
+                        act_s = nas;
+                        lam = nlam;
+                    }
+                    --k;
+                    cdrop = ci;
+                    q = m0 + ci;
+                    rebuild = true;
+                    need_select = false;
                 }
-                __syncthreads();
+                if (iters >= maxit && go) {
+                    status = 1;
+                    go = false;
+                }
+            }
+            S[L.U + i] = u_i;
+            __syncthreads();
+            if (__any(rebuild)) {
+                // Re-factor the inequality directions from the dropped position on: Q1T rows
+                // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
+                if (rebuild) {
+#pragma unroll
+                    for (int j = 0; j < NP; ++j)
+                        if (j >= cdrop) Tr.set(j, 0.0);
+                }
+                const int kk = rebuild ? k : 0;
+                int kmax = kk, amin = rebuild ? cdrop : NP;
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) {
+                    kmax = max(kmax, __shfl_xor(kmax, m, 64));
+                    amin = min(amin, __shfl_xor(amin, m, 64));
+                }
+                for (int a2 = amin; a2 < kmax; ++a2) {
+                    const bool on = rebuild && a2 >= cdrop && a2 < kk;
+                    const int pa = __shfl(act_p, a2, NP), sa = __shfl(act_s, a2, NP);
+                    const double nj = on ? sa * Mr.get(pa) : 0.0;
+                    S[L.NV + i] = nj;
+                    __syncthreads();
+                    const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
+                    const double zzr = isum<NP>(zr * zr);
+                    double rr2 = 0.0;
+                    if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
+                    if (on) {
+                        const double iz = frsq(zzr);
+                        S[L.QA + q * RS + i] = zr * iz;
+                        if (i < a2) Tr.set(a2, -rr2 * iz);
+                        if (i == a2) Tr.set(a2, iz);
+                        ++q;
+                    }
+                    __syncthreads();
+                }
             }
         }
-    }
 
-    // ------------------------------------------------------------ 5. output
-    const double x_i = Mr.dot(S + L.U, NP);
-    double tau_i = x_i + h_i;
-    if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
-    if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (QPPVMPlugin.cpp:246-249)
-    if (row) a.tau[bn + i] = tau_i;
-    if (valid && i == 0) {
-        a.status[b] = status;
-        a.iters[b] = iters;
+        const double x_i = Mr.dot(S + L.U, NP);
+        double tau_i = x_i + h_i;
+        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+        if (row) a.tau[bn + i] = tau_i;
+        if (valid && i == 0) {
+            a.status[b] = status;
+            a.iters[b] = iters;
+        }
+        __syncthreads();
     }
+    // the last block to finish resets the queue for the next solve
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int done = atomicAdd(a.qdone, 1);
+        if (done == (int)gridDim.x - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(a.qcount, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.qdone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int NP, typename Lay, typename K>
+hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t stream, size_t &attr_set)
+{
+    constexpr int IPW = kWave / NP;
+    const size_t lds = sizeof(double) * Lay(a.ntasks, a.m0).SIZE * IPW;
+    if (lds > attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, a);
+    return hipGetLastError();
 }
 
 template <int NP>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
 {
     constexpr int IPW = kWave / NP;
-    const size_t lds = sizeof(double) * Layout<NP>(a.ntasks).SIZE * IPW;
-    static size_t attr_set = 0;
-    if (lds > attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)qppvm_solve_kernel<NP>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = lds;
-    }
+    static size_t attr_fast = 0, attr_active = 0;
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(qppvm_solve_kernel<NP>, dim3(grid), dim3(kWave), lds, stream, a);
-    return hipGetLastError();
+    hipError_t e = launch_one<NP, FastLayout<NP>>(qppvm_fast_kernel<NP>, a, grid, stream, attr_fast);
+    if (e != hipSuccess) return e;
+    const unsigned grid_active = grid < kActiveBlocks ? grid : kActiveBlocks;
+    return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP>, a, grid_active, stream, attr_active);
 }
 
 }  // namespace

@@ -42,6 +42,9 @@ struct wbq_ctx {
     double t_acc_ms = 0.0;
     int t_launches = 0;
     std::string err;
+    unsigned long long *stamps = nullptr; // diagnostic builds only
+    double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
+    int *queue = nullptr, *qcount = nullptr;
 };
 
 namespace {
@@ -136,6 +139,18 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
          hipMemcpy(c->tmin, d.tau_min, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
          hipMemcpy(c->row_sel, sel, sizeof(int) * m0, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
+    {
+        const size_t np = (size_t)wbq::lanes_per_instance(d.n);
+        ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
+             hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
+             hipMalloc(&c->queue, B * 4) == hipSuccess && hipMalloc(&c->qcount, 16) == hipSuccess &&
+             hipMemset(c->qcount, 0, 16) == hipSuccess;
+        if (!ok) return cleanup(WBQ_E_DEVICE);
+    }
+#ifdef WBQ_STAMPS
+    if (hipMalloc(&c->stamps, sizeof(unsigned long long) * wbq::kStamps * B) != hipSuccess)
+        return cleanup(WBQ_E_DEVICE);
+#endif
     *out = c;
     return WBQ_SUCCESS;
 }
@@ -203,6 +218,12 @@ int wbq_solve(wbq_ctx *c)
     a.tau = c->out_tau ? c->out_tau : c->tau;
     a.status = c->out_status ? c->out_status : c->status;
     a.iters = c->out_iters ? c->out_iters : c->iters;
+    a.stamps = c->stamps;
+    a.u_scr = c->u_scr;
+    a.q1_scr = c->q1_scr;
+    a.queue = c->queue;
+    a.qcount = c->qcount;
+    a.qdone = c->qcount + 1;
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
@@ -296,6 +317,18 @@ int wbq_get_timing(wbq_ctx *c, double *total_ms, int *launches)
     return WBQ_SUCCESS;
 }
 
+#ifdef WBQ_STAMPS
+// Diagnostic-only symbol (not in include/wbq.h): per-block phase stamps of the last solve.
+int wbq_diag_stamps(wbq_ctx *c, unsigned long long *host, int nblocks)
+{
+    if (!c || !c->stamps) return WBQ_E_INVALID;
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    WBQ_HIP(hipMemcpy(host, c->stamps, sizeof(unsigned long long) * wbq::kStamps * nblocks,
+                      hipMemcpyDeviceToHost));
+    return WBQ_SUCCESS;
+}
+#endif
+
 void wbq_destroy(wbq_ctx *c)
 {
     if (!c) return;
@@ -310,6 +343,11 @@ void wbq_destroy(wbq_ctx *c)
     if (c->row_sel) (void)hipFree(c->row_sel);
     if (c->status) (void)hipFree(c->status);
     if (c->iters) (void)hipFree(c->iters);
+    if (c->stamps) (void)hipFree(c->stamps);
+    if (c->u_scr) (void)hipFree(c->u_scr);
+    if (c->q1_scr) (void)hipFree(c->q1_scr);
+    if (c->queue) (void)hipFree(c->queue);
+    if (c->qcount) (void)hipFree(c->qcount);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -25,7 +25,18 @@ struct QppvmArgs {
     double *tau;     // [B][n]
     int *status;     // [B]
     int *iters;      // [B]
+    unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [grid][kStamps] s_memtime
+    // fast kernel -> active-set kernel hand-off (device scratch sized for max_batch)
+    double *u_scr;   // [B][NP]
+    double *q1_scr;  // [B][kM0Max][NP]
+    int *queue;      // [B] instances needing active-set iterations
+    int *qcount;     // queue length (reset to 0 by the last active-set block)
+    int *qdone;      // active-set blocks finished
 };
+
+constexpr unsigned kActiveBlocks = 2048; // grid of the active-set kernel (grid-stride)
+
+constexpr int kStamps = 8;
 
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream);

@@ -1,0 +1,66 @@
+"""Diagnostics (GPU box): per-phase cycles from the stamp build, and launch time vs batch."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from qppvm_amd import wbq  # noqa: E402
+from qppvm_amd.problem import QPPVMProblem  # noqa: E402
+from qppvm_amd.synth import qppvm_instances, replicate  # noqa: E402
+
+PHASES = ["stage+force", "gauss-jordan", "equality block", "bound check+output"]
+
+
+def run(libpath, prob, inp, reps=20, stamps=False):
+    wbq._lib = None
+    wbq.load_library(libpath)
+    s = wbq.QPPVMSolver(prob, max_batch=inp["h"].shape[0])
+    s.set_inputs(inp)
+    s.solve()
+    s.sync()
+    s.set_timing(True)
+    for _ in range(reps):
+        s.solve()
+    ms, cnt = s.get_timing()
+    out = {"us_per_launch": 1e3 * ms / cnt}
+    if stamps:
+        B = inp["h"].shape[0]
+        nb = (B + 1) // 2 if prob.n <= 32 else B
+        buf = (ctypes.c_ulonglong * (8 * nb))()
+        s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        assert s.lib.wbq_diag_stamps(s.ctx, buf, nb) == 0
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8)[:, [0, 1, 2, 3, 5]].astype(np.int64)
+        d = np.diff(st, axis=1)
+        out["fast_kernel_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in enumerate(PHASES)}
+        out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
+    s.close()
+    return out
+
+
+def main():
+    from qppvm_amd import build
+    diag = build.build(force=True, diag=True)
+    res = {}
+    n = 30
+    base = qppvm_instances(QPPVMProblem(n=n), 65536, seed=1)
+    p1 = QPPVMProblem(n=n, tau_max=1e6)
+    for B in (256, 1024, 4096, 16384, 65536):
+        inp = replicate({k: v[:1] for k, v in base.items()}, B)
+        res[f"cfg1_B{B}"] = run(wbq.LIB_PATH, p1, inp)
+    inp = replicate({k: v[:1] for k, v in base.items()}, 4096)
+    res["cfg1_B4096_stamps"] = run(diag, p1, inp, stamps=True)
+    free = wbq.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=4096)
+    sub = {k: v[:4096] for k, v in base.items()}
+    tau_free, _, _ = free.solve_batch(sub)
+    free.close()
+    p2 = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
+    res["cfg2_B4096_stamps"] = run(diag, p2, sub, stamps=True)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
