@@ -119,112 +119,78 @@ static int lu_solve(int N, double *A, double *b, double rtol)
     return 0;
 }
 
-/* Cyclic Jacobi eigen-decomposition of a small symmetric matrix (A destroyed).
- * Eigenvalues in w, eigenvectors in the columns of V (row-major). */
-static void jacobi_eig(int N, double *A, double *V, double *w)
+/* One-sided Jacobi (Hestenes) SVD of X (R x C, row-major, C <= R is not required):
+ * orthogonalises the columns, X V = U diag(sig). On return X holds U diag(sig) (columns
+ * not normalised), V (C x C) the right singular vectors, sig the column norms. Singular
+ * values come out to relative accuracy, unlike eigenvalues of the Gram X^T X. */
+static void jacobi_svd(int R, int C, double *X, double *V, double *sig)
 {
-    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
-    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
-    for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0.0, diag = 0.0;
-        for (int i = 0; i < N; ++i) {
-            diag += A[i * N + i] * A[i * N + i];
-            for (int j = i + 1; j < N; ++j) off += A[i * N + j] * A[i * N + j];
-        }
-        if (off <= 1e-32 * dmax(diag, 1e-300)) break;
-        for (int p = 0; p < N; ++p)
-            for (int q = p + 1; q < N; ++q) {
-                const double apq = A[p * N + q];
-                if (apq == 0.0) continue;
-                const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < N; ++k) {
-                    const double akp = A[k * N + p], akq = A[k * N + q];
-                    A[k * N + p] = c * akp - s * akq;
-                    A[k * N + q] = s * akp + c * akq;
+    for (int i = 0; i < C * C; ++i) V[i] = 0.0;
+    for (int i = 0; i < C; ++i) V[i * C + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        int rotated = 0;
+        for (int p = 0; p < C; ++p)
+            for (int q = p + 1; q < C; ++q) {
+                double al = 0.0, be = 0.0, ga = 0.0;
+                for (int k = 0; k < R; ++k) {
+                    al += X[k * C + p] * X[k * C + p];
+                    be += X[k * C + q] * X[k * C + q];
+                    ga += X[k * C + p] * X[k * C + q];
                 }
-                for (int k = 0; k < N; ++k) {
-                    const double apk = A[p * N + k], aqk = A[q * N + k];
-                    A[p * N + k] = c * apk - s * aqk;
-                    A[q * N + k] = s * apk + c * aqk;
+                if (fabs(ga) <= 1e-15 * sqrt(al * be) || ga == 0.0) continue;
+                rotated = 1;
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                for (int k = 0; k < R; ++k) {
+                    const double xp = X[k * C + p], xq = X[k * C + q];
+                    X[k * C + p] = c * xp - sn * xq;
+                    X[k * C + q] = sn * xp + c * xq;
                 }
-                for (int k = 0; k < N; ++k) {
-                    const double vkp = V[k * N + p], vkq = V[k * N + q];
-                    V[k * N + p] = c * vkp - s * vkq;
-                    V[k * N + q] = s * vkp + c * vkq;
+                for (int k = 0; k < C; ++k) {
+                    const double vp = V[k * C + p], vq = V[k * C + q];
+                    V[k * C + p] = c * vp - sn * vq;
+                    V[k * C + q] = sn * vp + c * vq;
                 }
             }
+        if (!rotated) break;
     }
-    for (int i = 0; i < N; ++i) w[i] = A[i * N + i];
+    for (int j = 0; j < C; ++j) {
+        double s2 = 0.0;
+        for (int k = 0; k < R; ++k) s2 += X[k * C + j] * X[k * C + j];
+        sig[j] = sqrt(s2);
+    }
 }
 
-/* Pseudo-inverse apply for a small symmetric PSD matrix: out = G^+ r. */
-static void psd_pinv_apply(int N, const double *G, const double *r, double *out)
-{
-    double *A = (double *)malloc(sizeof(double) * N * N);
-    double *V = (double *)malloc(sizeof(double) * N * N);
-    double *w = (double *)malloc(sizeof(double) * N);
-    double *t = (double *)malloc(sizeof(double) * N);
-    memcpy(A, G, sizeof(double) * N * N);
-    jacobi_eig(N, A, V, w);
-    double wmax = 0.0;
-    for (int i = 0; i < N; ++i) wmax = dmax(wmax, fabs(w[i]));
-    const double cut = 1e-13 * wmax;
-    for (int k = 0; k < N; ++k) {
-        double s = 0.0;
-        for (int i = 0; i < N; ++i) s += V[i * N + k] * r[i];
-        t[k] = (w[k] > cut) ? s / w[k] : 0.0;
-    }
-    for (int i = 0; i < N; ++i) {
-        double s = 0.0;
-        for (int k = 0; k < N; ++k) s += V[i * N + k] * t[k];
-        out[i] = s;
-    }
-    free(A);
-    free(V);
-    free(w);
-    free(t);
-}
-
-/* Minimum-norm least squares over the columns F of A (m x n): z = argmin ||A_F z - r||, min ||z||. */
+/* Minimum-norm least squares over the columns F of A (m x n): z = pinv(A_F) r, via the SVD
+ * of A_F^T (k x m): A_F^T V = U S  =>  A_F = V S U^T  =>  pinv(A_F) = U S^-1 V^T. */
 static void minnorm_ls(int m, int n, const double *A, const int *F, int k, const double *r,
                        double *z)
 {
-    if (k >= m) {
-        double *G = (double *)calloc((size_t)m * m, sizeof(double));
-        double *s = (double *)malloc(sizeof(double) * m);
-        for (int a = 0; a < m; ++a)
-            for (int b = 0; b <= a; ++b) {
-                double t = 0.0;
-                for (int c = 0; c < k; ++c) t += A[a * n + F[c]] * A[b * n + F[c]];
-                G[a * m + b] = G[b * m + a] = t;
-            }
-        psd_pinv_apply(m, G, r, s);
-        for (int c = 0; c < k; ++c) {
-            double t = 0.0;
-            for (int a = 0; a < m; ++a) t += A[a * n + F[c]] * s[a];
-            z[c] = t;
-        }
-        free(G);
-        free(s);
-    } else {
-        double *G = (double *)calloc((size_t)k * k, sizeof(double));
-        double *s = (double *)malloc(sizeof(double) * k);
-        for (int a = 0; a < k; ++a) {
-            for (int b = 0; b <= a; ++b) {
-                double t = 0.0;
-                for (int i = 0; i < m; ++i) t += A[i * n + F[a]] * A[i * n + F[b]];
-                G[a * k + b] = G[b * k + a] = t;
-            }
-            double t = 0.0;
-            for (int i = 0; i < m; ++i) t += A[i * n + F[a]] * r[i];
-            s[a] = t;
-        }
-        psd_pinv_apply(k, G, s, z);
-        free(G);
-        free(s);
+    double *X = (double *)malloc(sizeof(double) * (k > 0 ? k : 1) * m);
+    double *V = (double *)malloc(sizeof(double) * m * m);
+    double *sig = (double *)malloc(sizeof(double) * m);
+    double *t = (double *)malloc(sizeof(double) * m);
+    for (int c = 0; c < k; ++c)
+        for (int a = 0; a < m; ++a) X[c * m + a] = A[a * n + F[c]];
+    jacobi_svd(k, m, X, V, sig);
+    double smax = 0.0;
+    for (int j = 0; j < m; ++j) smax = dmax(smax, sig[j]);
+    for (int j = 0; j < m; ++j) {
+        double s = 0.0;
+        for (int a = 0; a < m; ++a) s += V[a * m + j] * r[a];
+        /* U_j = X_j / sig_j, and z = sum_j U_j (V_j . r) / sig_j  => X_j (V_j . r) / sig_j^2 */
+        t[j] = (sig[j] > 1e-13 * smax) ? s / (sig[j] * sig[j]) : 0.0;
     }
+    for (int c = 0; c < k; ++c) {
+        double s = 0.0;
+        for (int j = 0; j < m; ++j) s += X[c * m + j] * t[j];
+        z[c] = s;
+    }
+    free(X);
+    free(V);
+    free(sig);
+    free(t);
 }
 
 /* ------------------------------------------------------------ task assembly */
@@ -534,7 +500,7 @@ int wbq_ref_level1(int n, const double *H, const double *g, int me, const double
     double *rhs = (double *)malloc(sizeof(double) * N);
     double *p = (double *)malloc(sizeof(double) * n);
     double *grad = (double *)malloc(sizeof(double) * n);
-    double *Gm = (double *)malloc(sizeof(double) * mq * mq);
+    double *Gm = (double *)malloc(sizeof(double) * mq * (n > mq ? n : mq));
     double *V = (double *)malloc(sizeof(double) * mq * mq);
     double *lam = (double *)malloc(sizeof(double) * mq);
     double *E2 = (double *)malloc(sizeof(double) * mq * n);
@@ -560,13 +526,10 @@ int wbq_ref_level1(int n, const double *H, const double *g, int me, const double
         /* independent equality rows on F */
         int r = 0;
         if (me > 0) {
-            for (int a = 0; a < me; ++a)
-                for (int b = 0; b <= a; ++b) {
-                    double t = 0.0;
-                    for (int c = 0; c < k; ++c) t += Aeq[a * n + F[c]] * Aeq[b * n + F[c]];
-                    Gm[a * me + b] = Gm[b * me + a] = t;
-                }
-            jacobi_eig(me, Gm, V, lam);
+            /* SVD of Aeq_F^T (k x me): the left singular vectors of Aeq_F are the columns of V */
+            for (int c = 0; c < k; ++c)
+                for (int a = 0; a < me; ++a) Gm[c * me + a] = Aeq[a * n + F[c]];
+            jacobi_svd(k, me, Gm, V, lam);
             double lmax = 0.0;
             for (int a = 0; a < me; ++a) lmax = dmax(lmax, lam[a]);
             for (int e = 0; e < me; ++e) {

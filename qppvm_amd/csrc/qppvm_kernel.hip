@@ -5,10 +5,11 @@
 //
 //   qppvm_fast_kernel    every instance: stage -> task forces -> Gauss-Jordan on M ->
 //                        equality-constrained optimum -> bound check -> tau. Instances whose
-//                        optimum violates a torque bound park (u, Q1) in scratch and append
-//                        themselves to a device work queue.
-//   qppvm_active_kernel  grid-stride over that queue only: Goldfarb-Idnani dual active set on
-//                        the torque bounds -> tau. Its last block resets the queue.
+//                        optimum violates a torque bound park (u, Q1) in scratch and mark
+//                        themselves with status -1.
+//   qppvm_active_kernel  same instance -> block mapping; blocks without a marked instance exit
+//                        at once, the others run the Goldfarb-Idnani dual active set on the
+//                        torque bounds -> tau.
 //
 // The split keeps the common path lean (VGPRs, LDS, hence occupancy) and gives the iterative
 // part its own resource budget.
@@ -300,7 +301,7 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 
 
 // ====================================================================== fast path
-template <int NP>
+template <int NP, int M0>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -461,61 +462,55 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         }
     }
     __syncthreads();
+    // Every lane factors the small Gram redundantly in registers (no cross-lane steps):
+    // rank-revealing Cholesky G G^T = L L^T (dependent rows get a zero column), then
+    // c = L^-T L^-1 (b0 - G u_imp), so that u_eq = u_imp + G^T c.
+    double Lm[M0 * (M0 + 1) / 2]; // packed lower triangle, row-major
+    double il[M0];
     {
-        // lane-parallel rank-revealing Cholesky G G^T = L L^T (lane r owns row r), fused with
-        // the forward substitution rho = L^-1 (b0 - G u_imp); dependent rows get a zero column
-        double g[kM0Max];
+        double dmx = 0.0;
 #pragma unroll
-        for (int c = 0; c < kM0Max; ++c) {
-            const int hi_ = i > c ? i : c, lo_ = i > c ? c : i;
-            g[c] = (i < m0 && c < m0) ? S[L.GR + hi_ * kM0Max + lo_] : 0.0;
+        for (int r = 0; r < M0; ++r) {
+#pragma unroll
+            for (int c = 0; c <= r; ++c) Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
+            dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
         }
-        double res = i < m0 ? S[L.RES + i] : 0.0;
-        double gdiag = 0.0;
 #pragma unroll
-        for (int c = 0; c < kM0Max; ++c) gdiag = (c == i) ? g[c] : gdiag;
-        const double dmx = imax<NP>(gdiag);
+        for (int c = 0; c < M0; ++c) {
+            double d = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
-        for (int c = 0; c < kM0Max; ++c) {
-            if (c < m0) {
-                const double dc = __shfl(g[c], c, NP);
-                const bool indep = dc > 1e-12 * dmx;
-                const double il = indep ? frsq(dc) : 0.0; // 1 / L_cc
-                const double lrc = (i > c) ? g[c] * il : (i == c ? dc * il : 0.0);
-                const double rho_c = __shfl(res, c, NP) * il;
-                if (i > c) res = fma(-lrc, rho_c, res);
-                if (i == c) {
-                    S[L.RHO + c] = rho_c;
-                    S[L.ID + c] = il;
-                }
-                if (i < m0) {
-                    S[L.LC + i] = lrc;
-                    S[L.GR + i * kM0Max + c] = lrc;
-                }
-                __syncthreads();
+            for (int k = 0; k < c; ++k) d = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], d);
+            const bool indep = c < m0 && d > 1e-12 * dmx;
+            const double ic_ = indep ? frsq(d) : 0.0;
+            il[c] = ic_;
+            Lm[c * (c + 1) / 2 + c] = d * ic_;
 #pragma unroll
-                for (int j = c + 1; j < kM0Max; ++j) g[j] = fma(-lrc, S[L.LC + j], g[j]);
+            for (int r = c + 1; r < M0; ++r) {
+                double t = Lm[r * (r + 1) / 2 + c];
+#pragma unroll
+                for (int k = 0; k < c; ++k) t = fma(-Lm[r * (r + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], t);
+                Lm[r * (r + 1) / 2 + c] = t * ic_;
             }
         }
     }
-    __syncthreads();
-    // c = L^-T rho (every lane, from LDS broadcasts), u_eq = u_imp + G^T c
-    double cv[kM0Max];
+    double cv[M0];
 #pragma unroll
-    for (int c = kM0Max - 1; c >= 0; --c) {
-        double v = 0.0;
-        if (c < m0) {
-            v = S[L.RHO + c];
+    for (int c = 0; c < M0; ++c) { // forward: rho = L^-1 res
+        double v = (c < m0) ? S[L.RES + c] : 0.0;
 #pragma unroll
-            for (int k = c + 1; k < kM0Max; ++k)
-                if (k < m0) v = fma(-S[L.GR + k * kM0Max + c], cv[k], v);
-            v *= S[L.ID + c];
-        }
-        cv[c] = v;
+        for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], cv[k], v);
+        cv[c] = v * il[c];
+    }
+#pragma unroll
+    for (int c = M0 - 1; c >= 0; --c) { // backward: c = L^-T rho
+        double v = cv[c];
+#pragma unroll
+        for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
+        cv[c] = v * il[c];
     }
     double u_i = u_imp;
 #pragma unroll
-    for (int c = 0; c < kM0Max; ++c)
+    for (int c = 0; c < M0; ++c)
         if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
     S[L.U + i] = u_i;
     __syncthreads();
@@ -562,31 +557,27 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         }
     } else {
         // park (u, Q1) for the active-set kernel; Q1 = G^T L^-T row by row
-        double q1[kM0Max];
+        double q1[M0];
 #pragma unroll
-        for (int c = 0; c < kM0Max; ++c) {
-            double v = 0.0;
-            if (c < m0) {
-                v = S[L.JR + a.row_sel[c] * NP + i];
+        for (int c = 0; c < M0; ++c) {
+            double v = (c < m0) ? S[L.JR + a.row_sel[c] * NP + i] : 0.0;
 #pragma unroll
-                for (int k = 0; k < c; ++k) v = fma(-S[L.GR + c * kM0Max + k], q1[k], v);
-                v *= S[L.ID + c];
-            }
-            q1[c] = v;
+            for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], q1[k], v);
+            q1[c] = v * il[c];
         }
         double *us = a.u_scr + b * NP;
         double *qs = a.q1_scr + b * kM0Max * NP;
         us[i] = u_i;
 #pragma unroll
-        for (int c = 0; c < kM0Max; ++c)
+        for (int c = 0; c < M0; ++c)
             if (c < m0) qs[c * NP + i] = q1[c];
-        if (i == 0) a.queue[atomicAdd(a.qcount, 1)] = (int)b;
+        if (i == 0) a.status[b] = -1; // picked up by the active-set kernel
     }
     WBQ_STAMP(5);
 }
 
 // ============================================================== active-set path
-template <int NP>
+template <int NP, int M0>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -599,15 +590,15 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     const int sub = tid / NP;
     const int i = tid - sub * NP;
     double *S = smem + sub * L.SIZE;
-    const int count = __hip_atomic_load(a.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long Bn = (long)a.B * n;
     const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
     const int ic = i < n ? i : n - 1;
-
-    for (int base = blockIdx.x * IPW; base < count; base += gridDim.x * IPW) {
-        const int e = base + sub;
-        const bool valid = e < count;
-        const long b = valid ? a.queue[e] : 0;
+    {
+        const long b0_ = (long)blockIdx.x * IPW + sub;
+        // instances the fast kernel parked (status -1); blocks with none exit at once
+        const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
+        if (!__any(valid)) return;
+        const long b = valid ? b0_ : 0;
         const bool row = valid && i < n;
         const long bn = b * n;
         const int moff = (int)(8 * (b * n * n + ic));
@@ -633,7 +624,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         const double *qs = a.q1_scr + b * kM0Max * NP;
 #pragma unroll
         for (int c = 0; c < NP; ++c)
-            S[L.QA + c * RS + i] = (valid && c < kM0Max && c < m0) ? qs[(c < kM0Max ? c : 0) * NP + i] : 0.0;
+            S[L.QA + c * RS + i] = (valid && c < M0 && c < m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
         S[L.D1 + NP + i] = 0.0;
         S[L.U + i] = u_i;
         RowStore<NP, MREG> Tr;
@@ -782,17 +773,6 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             a.status[b] = status;
             a.iters[b] = iters;
         }
-        __syncthreads();
-    }
-    // the last block to finish resets the queue for the next solve
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int done = atomicAdd(a.qdone, 1);
-        if (done == (int)gridDim.x - 1) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(a.qcount, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.qdone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
@@ -810,25 +790,24 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
     return hipGetLastError();
 }
 
-template <int NP>
+template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
 {
     constexpr int IPW = kWave / NP;
     static size_t attr_fast = 0, attr_active = 0;
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
-    hipError_t e = launch_one<NP, FastLayout<NP>>(qppvm_fast_kernel<NP>, a, grid, stream, attr_fast);
+    hipError_t e = launch_one<NP, FastLayout<NP>>(qppvm_fast_kernel<NP, M0>, a, grid, stream, attr_fast);
     if (e != hipSuccess) return e;
-    const unsigned grid_active = grid < kActiveBlocks ? grid : kActiveBlocks;
-    return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP>, a, grid_active, stream, attr_active);
+    return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
 }
 
 }  // namespace
 
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream)
 {
-    if (a.n <= 32) return launch_np<32>(a, stream);
-    return launch_np<64>(a, stream);
+    if (a.n <= 32) return a.m0 <= 6 ? launch_np<32, 6>(a, stream) : launch_np<32, kM0Max>(a, stream);
+    return a.m0 <= 6 ? launch_np<64, 6>(a, stream) : launch_np<64, kM0Max>(a, stream);
 }
 
 }  // namespace wbq

@@ -44,7 +44,6 @@ struct wbq_ctx {
     std::string err;
     unsigned long long *stamps = nullptr; // diagnostic builds only
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
-    int *queue = nullptr, *qcount = nullptr;
 };
 
 namespace {
@@ -142,9 +141,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     {
         const size_t np = (size_t)wbq::lanes_per_instance(d.n);
         ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
-             hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
-             hipMalloc(&c->queue, B * 4) == hipSuccess && hipMalloc(&c->qcount, 16) == hipSuccess &&
-             hipMemset(c->qcount, 0, 16) == hipSuccess;
+             hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess;
         if (!ok) return cleanup(WBQ_E_DEVICE);
     }
 #ifdef WBQ_STAMPS
@@ -221,9 +218,7 @@ int wbq_solve(wbq_ctx *c)
     a.stamps = c->stamps;
     a.u_scr = c->u_scr;
     a.q1_scr = c->q1_scr;
-    a.queue = c->queue;
-    a.qcount = c->qcount;
-    a.qdone = c->qcount + 1;
+
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
@@ -346,8 +341,7 @@ void wbq_destroy(wbq_ctx *c)
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->u_scr) (void)hipFree(c->u_scr);
     if (c->q1_scr) (void)hipFree(c->q1_scr);
-    if (c->queue) (void)hipFree(c->queue);
-    if (c->qcount) (void)hipFree(c->qcount);
+
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

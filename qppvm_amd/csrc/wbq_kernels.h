@@ -26,15 +26,11 @@ struct QppvmArgs {
     int *status;     // [B]
     int *iters;      // [B]
     unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [grid][kStamps] s_memtime
-    // fast kernel -> active-set kernel hand-off (device scratch sized for max_batch)
+    // fast kernel -> active-set kernel hand-off (device scratch sized for max_batch); the
+    // fast kernel marks an instance that needs active-set steps with status -1
     double *u_scr;   // [B][NP]
     double *q1_scr;  // [B][kM0Max][NP]
-    int *queue;      // [B] instances needing active-set iterations
-    int *qcount;     // queue length (reset to 0 by the last active-set block)
-    int *qdone;      // active-set blocks finished
 };
-
-constexpr unsigned kActiveBlocks = 2048; // grid of the active-set kernel (grid-stride)
 
 constexpr int kStamps = 8;
 
