@@ -57,24 +57,20 @@ constexpr double kInf = 1.0e300;
 // NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
 template <int NP>
 struct FastLayout {
-    int JR, BC, RH, U, WV, QD, F, B0, RES, RHO, CV, GR, ID, LC, PS, SIZE;
+    static constexpr int BS = 4; // Gauss-Jordan pivot block
+    int JR, PN, RH, U, WV, QD, F, RES, GR, PS, SIZE;
     __host__ __device__ FastLayout(int T, int m0)
     {
         JR = 0;                  // J rows [T*6][NP]
-        BC = JR + T * 6 * NP;    // GJ pivot column, double-buffered [2][NP]
-        RH = BC + 2 * NP;        // GJ pivot right-hand sides [2][8]
-        U = RH + 16;             // u
-        WV = U + NP;             // w_t [T][NP]
+        PN = JR + T * 6 * NP;    // pivot panel, double-buffered [2][NP][BS]
+        RH = PN + 2 * NP * BS;   // right-hand sides of the pivot rows [2][BS][8]
+        U = RH + 2 * BS * 8;     // u
+        WV = U + NP;             // w_t - u_imp [T][NP]
         QD = WV + T * NP;        // qdot
         F = QD + NP;             // task forces [T*6]
-        B0 = F + 6 * T;          // b0 [m0]
-        RES = B0 + m0;           // b0 - G u_imp
-        RHO = RES + m0;          // L^-1 (b0 - G u_imp)
-        CV = RHO + m0;           // L^-T rho
-        GR = CV + m0;            // Gram, then its Cholesky factor L [m0][kM0Max]
-        ID = GR + m0 * kM0Max;   // 1 / L_cc (0 for dependent rows)
-        LC = ID + kM0Max;        // broadcast column of L
-        PS = LC + kM0Max;        // poses [T][24]
+        RES = F + 6 * T;         // b0 - G u_imp [m0]
+        GR = RES + m0;           // Gram G G^T, lower triangle [m0][kM0Max]
+        PS = GR + m0 * kM0Max;   // poses [T][24]
         SIZE = (PS + 24 * T + 1) & ~1;
     }
 };
@@ -375,7 +371,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     __syncthreads();
     WBQ_STAMP(1);
 
-    // ------------------------------------------------- 2. Gauss-Jordan, M SPD
+    // ------------------------------------------ 2. block Gauss-Jordan, M SPD
     double rhs[1 + kTMax];
     rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
 #pragma unroll
@@ -386,104 +382,166 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
         rhs[1 + t] = c; // J_t^T F_t
     }
-    double dval = 1.0;
+    // Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing
+    // Schur complement stays symmetric: pivot row k+r, column j, equals lane j's entry in
+    // column k+r. Every lane publishes its BS panel entries; every lane factors the BS x BS
+    // pivot block D redundantly and applies one rank-BS update:
+    //   rows outside the block: row -= (a_i D^-1) P,   rows inside: row = (D^-1)_ri P,
+    // so each row ends up normalised by its own pivot block (x_i = rhs_i, no division).
+    // The next panel is updated and published first (lookahead), then the rest of the row.
+    constexpr int BS = FastLayout<NP>::BS;
     bool notspd = false;
-    // M SPD: no pivoting, and the trailing block stays symmetric, so the pivot row is the
-    // pivot column every lane publishes. Step k reads buffer k&1 and publishes column k+1
-    // into the other buffer as soon as it is updated (lookahead).
-    S[L.BC + i] = A[0];
-    if (i == 0) {
+    {
+        double *pn0 = S + L.PN;
 #pragma unroll
-        for (int m = 0; m < 1 + kTMax; ++m) S[L.RH + m] = rhs[m];
+        for (int c = 0; c < BS; ++c) pn0[i * BS + c] = A[c];
+        if (i < BS) {
+#pragma unroll
+            for (int m = 0; m < 1 + kTMax; ++m) S[L.RH + i * 8 + m] = rhs[m];
+        }
     }
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
+    for (int kb = 0; kb < NP / BS; ++kb) {
+        const int k = kb * BS;
         if (k < n) {
             __syncthreads();
-            const double *bc = S + L.BC + (k & 1) * NP;
-            const double *rh = S + L.RH + (k & 1) * 8;
-            double *bcn = S + L.BC + ((k + 1) & 1) * NP;
-            double *rhn = S + L.RH + ((k + 1) & 1) * 8;
-            const double piv = bc[k];
-            notspd |= !(piv > 0.0);
-            const double f = (i == k) ? 0.0 : A[k] * frcp(piv);
+            const double *pn = S + L.PN + (kb & 1) * NP * BS;
+            const double *rh = S + L.RH + (kb & 1) * BS * 8;
+            double *pnn = S + L.PN + ((kb + 1) & 1) * NP * BS;
+            double *rhn = S + L.RH + ((kb + 1) & 1) * BS * 8;
+            // Cholesky of the pivot block (redundant per lane)
+            double d[BS][BS];
 #pragma unroll
-            for (int m = 0; m < 1 + kTMax; ++m) rhs[m] = fma(-f, rh[m], rhs[m]);
-            if (k + 1 < NP) {
-                A[k + 1] = fma(-f, bc[k + 1], A[k + 1]);
-                if (k + 1 < n) {
-                    bcn[i] = A[k + 1];
-                    if (i == k + 1) {
+            for (int r = 0; r < BS; ++r)
 #pragma unroll
-                        for (int m = 0; m < 1 + kTMax; ++m) rhn[m] = rhs[m];
-                    }
+                for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
+            double il[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double dd = d[c][c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
+                notspd |= !(dd > 0.0);
+                il[c] = frsq(dd);
+#pragma unroll
+                for (int r = c + 1; r < BS; ++r) {
+                    double t = d[r][c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
+                    d[r][c] = t * il[c];
+                }
+            }
+            // solve D y = e, e = unit(i-k) for the block's own rows, else a_i = row i's panel
+            const int ri = i - k;
+            const bool inK = ri >= 0 && ri < BS;
+            double y[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double v = inK ? (ri == c ? 1.0 : 0.0) : A[k + c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
+                y[c] = v * il[c];
+            }
+#pragma unroll
+            for (int c = BS - 1; c >= 0; --c) {
+                double v = y[c];
+#pragma unroll
+                for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
+                y[c] = v * il[c];
+            }
+            const double cc = inK ? 0.0 : 1.0;
+            double hh[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) hh[c] = inK ? y[c] : -y[c];
+#pragma unroll
+            for (int m = 0; m < 1 + kTMax; ++m) {
+                double v = cc * rhs[m];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], rh[c * 8 + m], v);
+                rhs[m] = v;
+            }
+            // lookahead: next panel first
+#pragma unroll
+            for (int j = k + BS; j < k + 2 * BS && j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
+            if (k + BS < n) {
+#pragma unroll
+                for (int c = 0; c < BS; ++c)
+                    if (k + BS + c < NP) pnn[i * BS + c] = A[(k + BS + c) < NP ? k + BS + c : NP - 1];
+                const int rn = i - (k + BS);
+                if (rn >= 0 && rn < BS) {
+#pragma unroll
+                    for (int m = 0; m < 1 + kTMax; ++m) rhn[rn * 8 + m] = rhs[m];
                 }
             }
 #pragma unroll
-            for (int j = k + 2; j < NP; ++j) A[j] = fma(-f, bc[j], A[j]);
-            dval = (i == k) ? piv : dval;
+            for (int j = k + 2 * BS; j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
         }
     }
-    const double dinv = frcp(dval);
-    const double u_imp = rhs[0] * dinv;
-    S[L.U + i] = u_imp;
+    const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
 #pragma unroll
     for (int t = 0; t < kTMax; ++t)
-        if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] * dinv; // w_t = M^-1 J_t^T F_t
+        if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
     __syncthreads();
     WBQ_STAMP(2);
 
     // ------------------------------ 3. level-0 rows: G u = b0 in least distance from u_imp
-    if (i < m0) {
-        const int rr = a.row_sel[i], t = rr / 6;
-        double bb = 0.0, gu = 0.0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            const double g = S[L.JR + rr * NP + j];
-            bb = fma(g, S[L.WV + t * NP + j], bb);
-            gu = fma(g, S[L.U + j], gu);
-        }
-        S[L.B0 + i] = bb;          // b0 = S J M^-1 J^T F
-        S[L.RES + i] = bb - gu;
-    }
+    // res_a = b0_a - G_a u_imp = G_a (w_t(a) - u_imp), and the Gram G G^T: one dot per lane
     {
-        // Gram G G^T, lower triangle: one (row, col) pair per lane
         const int npairs = m0 * (m0 + 1) / 2;
-        for (int pp = i; pp < npairs; pp += NP) {
-            int ra = (int)((sqrtf(8.0f * pp + 1.0f) - 1.0f) * 0.5f);
-            ra += ((ra + 1) * (ra + 2) / 2 <= pp) ? 1 : 0;
-            ra -= (ra * (ra + 1) / 2 > pp) ? 1 : 0;
-            const int ca = pp - ra * (ra + 1) / 2;
-            const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
-            double g = 0.0;
+        for (int pp = i; pp < npairs + m0; pp += NP) {
+            if (pp < m0) {
+                const int rr = a.row_sel[pp], t = rr / 6;
+                double v = 0.0;
 #pragma unroll
-            for (int j = 0; j < NP; ++j) g = fma(S[L.JR + r1 * NP + j], S[L.JR + r2 * NP + j], g);
-            S[L.GR + ra * kM0Max + ca] = g;
+                for (int j = 0; j < NP; ++j) v = fma(S[L.JR + rr * NP + j], S[L.WV + t * NP + j], v);
+                S[L.RES + pp] = v;
+            } else {
+                const int p2 = pp - m0;
+                int ra = (int)((sqrtf(8.0f * p2 + 1.0f) - 1.0f) * 0.5f);
+                ra += ((ra + 1) * (ra + 2) / 2 <= p2) ? 1 : 0;
+                ra -= (ra * (ra + 1) / 2 > p2) ? 1 : 0;
+                const int ca = p2 - ra * (ra + 1) / 2;
+                const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
+                double g = 0.0;
+#pragma unroll
+                for (int j = 0; j < NP; ++j) g = fma(S[L.JR + r1 * NP + j], S[L.JR + r2 * NP + j], g);
+                S[L.GR + ra * kM0Max + ca] = g;
+            }
         }
     }
     __syncthreads();
-    // Every lane factors the small Gram redundantly in registers (no cross-lane steps):
-    // rank-revealing Cholesky G G^T = L L^T (dependent rows get a zero column), then
-    // c = L^-T L^-1 (b0 - G u_imp), so that u_eq = u_imp + G^T c.
+    // Every lane factors the small Gram redundantly in registers: rank-revealing Cholesky
+    // G G^T = L L^T (dependent rows get a zero column), c = L^-T L^-1 res, u = u_imp + G^T c.
     double Lm[M0 * (M0 + 1) / 2]; // packed lower triangle, row-major
-    double il[M0];
+    double il[M0], rs[M0];
     {
         double dmx = 0.0;
 #pragma unroll
         for (int r = 0; r < M0; ++r) {
+            rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
 #pragma unroll
             for (int c = 0; c <= r; ++c) Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
             dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
         }
 #pragma unroll
         for (int c = 0; c < M0; ++c) {
-            double d = Lm[c * (c + 1) / 2 + c];
+            double dd = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
-            for (int k = 0; k < c; ++k) d = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], d);
-            const bool indep = c < m0 && d > 1e-12 * dmx;
-            const double ic_ = indep ? frsq(d) : 0.0;
+            for (int k = 0; k < c; ++k) dd = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], dd);
+            const bool indep = c < m0 && dd > 1e-12 * dmx;
+            const double ic_ = indep ? frsq(dd) : 0.0;
             il[c] = ic_;
-            Lm[c * (c + 1) / 2 + c] = d * ic_;
+            Lm[c * (c + 1) / 2 + c] = dd * ic_;
 #pragma unroll
             for (int r = c + 1; r < M0; ++r) {
                 double t = Lm[r * (r + 1) / 2 + c];
@@ -496,7 +554,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     double cv[M0];
 #pragma unroll
     for (int c = 0; c < M0; ++c) { // forward: rho = L^-1 res
-        double v = (c < m0) ? S[L.RES + c] : 0.0;
+        double v = rs[c];
 #pragma unroll
         for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], cv[k], v);
         cv[c] = v * il[c];
@@ -508,47 +566,51 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
         cv[c] = v * il[c];
     }
+    // re-read M's rows (L2-hot) for the bound check; the latency hides under what follows
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    // consistency of the level-0 rows (rows dropped as dependent must still be met,
+    // otherwise y* != b0: level 0 infeasible)
+    double eqres = 0.0, rmx = 1.0;
+#pragma unroll
+    for (int r = 0; r < M0; ++r) {
+        double v = -rs[r];
+#pragma unroll
+        for (int c = 0; c < M0; ++c)
+            if (r < m0 && c < m0) v = fma(S[L.GR + (r >= c ? r * kM0Max + c : c * kM0Max + r)], cv[c], v);
+        eqres = fmax(eqres, fabs(v));
+        rmx = fmax(rmx, fabs(rs[r]));
+    }
     double u_i = u_imp;
 #pragma unroll
     for (int c = 0; c < M0; ++c)
         if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
     S[L.U + i] = u_i;
     __syncthreads();
-    // residual of every level-0 row (catches rows dropped as dependent: level 0 infeasible)
-    double eqres = 0.0;
-    if (i < m0) {
-        const int rr = a.row_sel[i];
-        double gu = 0.0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) gu = fma(S[L.JR + rr * NP + j], S[L.U + j], gu);
-        const double bb = S[L.B0 + i];
-        eqres = fabs(gu - bb) / fmax(1.0, fabs(bb));
-    }
-    eqres = imax<NP>(eqres);
     WBQ_STAMP(3);
 
     // ------------------------------------------------------------ 4. bound check
-    // x = M u with M's rows re-read (coalesced, L2-hot) into the registers A freed
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     double x_i = 0.0;
 #pragma unroll
     for (int r = 0; r < NP; ++r) x_i = fma((row && r < n) ? A[r] : (r == i ? 1.0 : 0.0), S[L.U + r], x_i);
     const double lo = row ? a.tau_min[ic] - h_i : -kInf;
     const double hi = row ? a.tau_max[ic] - h_i : kInf;
     int status = 0;
-    if (imax<NP>((row && lo > hi) ? 1.0 : 0.0) > 0.0) status = 2; // crossed limits
-    if (imax<NP>(notspd ? 1.0 : 0.0) > 0.0) status = 3;
-    if (status == 0 && eqres > 1e-9) status = 2; // level 0 infeasible
-    double viol = 0.0;
+    if (a.limits_crossed) status = 2; // tau_min > tau_max somewhere: infeasible everywhere
+    if (notspd) status = 3;           // (instance-uniform: pivots are broadcast values)
+    if (status == 0 && eqres > 1e-9 * rmx) status = 2; // level 0 infeasible
+    double flag = 0.0;
     if (row) {
         const double tol = 1e-10 * fmax(1.0, fmax(fabs(x_i), fmax(fabs(lo), fabs(hi))));
-        if (fmax(lo - x_i, x_i - hi) > tol) viol = 1.0;
+        if (fmax(lo - x_i, x_i - hi) > tol) flag = 1.0;
+        if (!isfinite(x_i)) flag = 2.0;
     }
-    const bool active = imax<NP>(viol) > 0.0 && status == 0 && valid;
+    flag = imax<NP>(flag);
+    if (flag >= 2.0 && status == 0) status = 3;
+    const bool active = flag > 0.0 && status == 0 && valid;
+
     if (!active) {
         double tau_i = x_i + h_i;
-        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
         if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
         if (row) a.tau[bn + i] = tau_i;
         if (valid && i == 0) {
@@ -598,6 +660,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         // instances the fast kernel parked (status -1); blocks with none exit at once
         const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
         if (!__any(valid)) return;
+        WBQ_STAMP(4);
         const long b = valid ? b0_ : 0;
         const bool row = valid && i < n;
         const long bn = b * n;
@@ -645,6 +708,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         double lamp = 0.0;
         bool need_select = true;
         const int maxit = a.max_iter;
+        WBQ_STAMP(6);
 
         while (true) {
             const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
@@ -773,6 +837,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             a.status[b] = status;
             a.iters[b] = iters;
         }
+        WBQ_STAMP(7);
     }
 }
 

@@ -18,6 +18,7 @@ struct wbq_ctx {
     int device = 0;
     wbq_desc d{};
     int m0 = 0;
+    int limits_crossed = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // batch-shared parameters (device)
@@ -114,6 +115,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     if (c->d.max_iter <= 0) c->d.max_iter = 4 * d.n + 32;
     c->m0 = m0;
     c->device = device;
+    for (int j = 0; j < d.n; ++j)
+        if (d.tau_min[j] > d.tau_max[j]) c->limits_crossed = 1;
     auto cleanup = [&](int rc) {
         wbq_destroy(c);
         return rc;
@@ -196,6 +199,7 @@ int wbq_solve(wbq_ctx *c)
     a.m0 = c->m0;
     a.select_mode = c->d.select_mode;
     a.max_iter = c->d.max_iter;
+    a.limits_crossed = c->limits_crossed;
     for (int t = 0; t < wbq::kTMax; ++t) a.row_mask[t] = t < c->d.ntasks ? c->d.row_mask[t] : 0;
     a.row_sel = c->row_sel;
     a.Kc = c->Kc;

@@ -16,6 +16,7 @@ struct QppvmArgs {
     int m0;          // level-0 rows (selected task rows)
     int select_mode; // WBQ_SELECT_*
     int max_iter;    // active-set step cap
+    int limits_crossed; // some tau_min > tau_max (batch-shared limits): every instance infeasible
     int row_mask[kTMax];
     const int *row_sel;      // [m0] task-row index t*6+r of level-0 row a (device)
     const double *Kc, *Dc;   // [ntasks*6] (device)

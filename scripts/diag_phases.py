@@ -37,6 +37,19 @@ def run(libpath, prob, inp, reps=20, stamps=False):
         d = np.diff(st, axis=1)
         out["fast_kernel_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in enumerate(PHASES)}
         out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
+        full = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
+        _, status, iters = s.outputs()
+        it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if prob.n <= 32 else iters[:nb]
+        act = it_blk > 0
+        if act.any():
+            setup = full[act, 6] - full[act, 4]
+            loop = full[act, 7] - full[act, 6]
+            out["active_blocks"] = int(act.sum())
+            out["active_setup_cycles_mean"] = float(setup.mean())
+            out["active_loop_cycles_mean"] = float(loop.mean())
+            out["active_cycles_per_step_mean"] = float((loop / it_blk[act]).mean())
+            out["active_block_max_steps_p50_p90_max"] = [float(np.percentile(it_blk[act], q)) for q in (50, 90, 100)]
+            out["iters_hist"] = np.bincount(iters).tolist()
     s.close()
     return out
 
