@@ -40,5 +40,32 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     return lib
 
 
+PLUGIN_DIR = os.path.join(HERE, "plugins")
+PLUGIN_LIB = os.path.join(HERE, "libQPPVMPlugin.so")
+DRIVER = os.path.join(HERE, "qppvm_dummy_driver")
+
+
+def build_plugins(verbose: bool = False) -> tuple:
+    """The XBot plugin shell (libQPPVMPlugin.so, same target name as the reference's
+    CMakeLists.txt:48) and the config-0 dummy-mode driver, host C++ over libwbq.so."""
+    build()
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(PLUGIN_DIR, "compat"),
+           "-I", os.path.join(PLUGIN_DIR, "include"), "-I", os.path.join(PLUGIN_DIR, "src")]
+    link = ["-L", HERE, "-lwbq", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"]
+    src = os.path.join(PLUGIN_DIR, "src", "QPPVMPlugin.cpp")
+    cmds = [
+        ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", *inc, src, "-o", PLUGIN_LIB, *link],
+        ["g++", "-O2", "-std=c++17", "-Wall", *inc, os.path.join(PLUGIN_DIR, "src", "dummy_driver.cpp"), src,
+         "-o", DRIVER, *link],
+    ]
+    for c in cmds:
+        if verbose:
+            print(" ".join(c), file=sys.stderr)
+        subprocess.check_call(c)
+    return PLUGIN_LIB, DRIVER
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))
+    if "--plugins" in sys.argv:
+        print(build_plugins(verbose=True))

@@ -368,12 +368,26 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
         S[L.F + i] = F;
     }
+    // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
+    // never has to be read again (a re-read of M would double the HBM bytes of the solve)
+    double Y[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        double v = 0.0;
+        if (c < m0) {
+            const int rr = a.row_sel[c];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+        }
+        Y[c] = v;
+    }
     __syncthreads();
     WBQ_STAMP(1);
 
     // ------------------------------------------ 2. block Gauss-Jordan, M SPD
     double rhs[1 + kTMax];
     rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
+    const double tau_imp_i = rhs[0];
 #pragma unroll
     for (int t = 0; t < kTMax; ++t) {
         double c = 0.0;
@@ -566,9 +580,6 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
         cv[c] = v * il[c];
     }
-    // re-read M's rows (L2-hot) for the bound check; the latency hides under what follows
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     // consistency of the level-0 rows (rows dropped as dependent must still be met,
     // otherwise y* != b0: level 0 infeasible)
     double eqres = 0.0, rmx = 1.0;
@@ -585,14 +596,12 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 #pragma unroll
     for (int c = 0; c < M0; ++c)
         if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
-    S[L.U + i] = u_i;
-    __syncthreads();
     WBQ_STAMP(3);
 
     // ------------------------------------------------------------ 4. bound check
-    double x_i = 0.0;
+    double x_i = tau_imp_i; // x = M u = tau_imp + M G^T c
 #pragma unroll
-    for (int r = 0; r < NP; ++r) x_i = fma((row && r < n) ? A[r] : (r == i ? 1.0 : 0.0), S[L.U + r], x_i);
+    for (int c = 0; c < M0; ++c) x_i = fma(Y[c], cv[c], x_i);
     const double lo = row ? a.tau_min[ic] - h_i : -kInf;
     const double hi = row ? a.tau_max[ic] - h_i : kInf;
     int status = 0;

@@ -1,0 +1,57 @@
+// QPPVMPlugin.h -- drop-in demo::QPPVMPlugin on the MI355X batched WBC-QP engine.
+//
+// Same class, namespace and XBot surface as the reference
+// (include/QPPVM_RT_plugin/QPPVMPlugin.h:35-46): init_control_plugin, on_start,
+// control_loop, close. What the reference delegates to OpenSoT (CartesianImpedanceCtrl x2,
+// JointImpedanceCtrl, TorqueLimits, AutoStack, QPOases_sot) goes through the wbq C ABI
+// (include/wbq.h); one wbq context per plugin, allocated in init_control_plugin.
+#pragma once
+
+#include <XCM/XBotControlPlugin.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "wbq.h"
+
+namespace demo {
+
+class QPPVMPlugin : public XBot::XBotControlPlugin {
+public:
+    QPPVMPlugin();
+    ~QPPVMPlugin() override;
+
+    bool init_control_plugin(XBot::Handle::Ptr handle) override;
+    void on_start(double time) override;
+    void control_loop(double time, double period) override;
+    bool close() override;
+
+    // observability (the reference logs these to MatLogger: tau_qp, tau_desired)
+    const Eigen::VectorXd &tau_desired() const { return _tau_d; }
+    int last_status() const { return _status; }
+    int solver_errors() const { return _solver_errors; }
+
+private:
+    void sense();
+    void syncFromMotorSide(XBot::RobotInterface::Ptr robot, XBot::ModelInterface::Ptr model);
+    void QPPVMControl(double time);
+
+    XBot::RobotInterface::Ptr _robot;
+    XBot::ModelInterface::Ptr _model;
+    wbq_ctx *_ctx = nullptr;
+
+    // task wiring (QPPVMPlugin.cpp:129-152): right arm then left arm, as in the stack sum
+    std::vector<std::string> _ee_links{"arm2_7", "arm1_7"};
+    double _start_time = 0.0;
+    int _status = 0;
+    int _solver_errors = 0;
+
+    Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h;
+    Eigen::VectorXd _tau_max_const, _tau_min_const;
+    Eigen::Affine3d _ref[2];
+    // per-tick input staging (instance-major, row-major: the wbq layout)
+    std::vector<double> _M, _J, _pose, _pose_ref;
+};
+
+}  // namespace demo

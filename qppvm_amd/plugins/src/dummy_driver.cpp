@@ -1,0 +1,100 @@
+// dummy_driver.cpp -- BASELINE config 0: the QPPVM plugin in an XBotCore-like dummy loop.
+// init_control_plugin -> on_start -> N x control_loop (period 1 ms) -> close, on the
+// synthetic robot of dummy_robot.h. Reports us/tick; optionally dumps the first ticks'
+// solver inputs and torques (binary, for the oracle parity test).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include <QPPVM_RT_plugin/QPPVMPlugin.h>
+
+#include "dummy_robot.h"
+
+int main(int argc, char **argv)
+{
+    int ticks = 10000, dump_ticks = 0, n = 39;
+    const char *dump = nullptr;
+    for (int k = 1; k < argc; ++k) {
+        if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
+        else if (!std::strcmp(argv[k], "--n") && k + 1 < argc) n = std::atoi(argv[++k]);
+        else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
+            dump = argv[++k];
+            dump_ticks = std::atoi(argv[++k]);
+        }
+    }
+    dummy::Params prm;
+    prm.n = n;
+    auto handle = std::make_shared<dummy::Handle>(prm);
+    demo::QPPVMPlugin plugin;
+    if (!plugin.init_control_plugin(handle)) {
+        std::fprintf(stderr, "init_control_plugin failed\n");
+        return 2;
+    }
+    FILE *f = dump ? std::fopen(dump, "wb") : nullptr;
+    const double dt = 1e-3;
+    plugin.on_start(0.0);
+    if (f) {
+        // header: n, ticks, then the references fixed at on_start (q_ref, pose_ref x2)
+        const int hdr[2] = {n, dump_ticks};
+        std::fwrite(hdr, sizeof(int), 2, f);
+        Eigen::VectorXd q;
+        handle->model().getJointPosition(q);
+        std::fwrite(q.data(), sizeof(double), n, f);
+        for (const char *link : {"arm2_7", "arm1_7"}) {
+            Eigen::Affine3d P;
+            handle->model().getPose(link, P);
+            std::fwrite(P.m, sizeof(double), 12, f);
+        }
+    }
+    // the references are the start posture; kick the robot so the tasks have work to do
+    {
+        Eigen::VectorXd q(n, 0.0), qd(n, 0.0);
+        for (int j = 0; j < n; ++j) qd[j] = 0.2 * ((j % 7) - 3);
+        handle->robot().set_state(q, qd);
+    }
+    double worst = 0.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < ticks; ++k) {
+        const double time = (k + 1) * dt;
+        const auto a = std::chrono::steady_clock::now();
+        plugin.run(time, dt);
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+        worst = us > worst ? us : worst;
+        if (f && k < dump_ticks) {
+            // the solver inputs of this tick, recomputed from the (unchanged) model state
+            auto &m = handle->model();
+            Eigen::MatrixXd M, J;
+            Eigen::VectorXd q, qd, h, tau = plugin.tau_desired();
+            m.getInertiaMatrix(M);
+            m.getJointPosition(q);
+            m.getJointVelocity(qd);
+            m.computeNonlinearTerm(h);
+            std::fwrite(M.data(), sizeof(double), (size_t)n * n, f);
+            for (const char *link : {"arm2_7", "arm1_7"}) {
+                m.getJacobian(link, J);
+                std::fwrite(J.data(), sizeof(double), (size_t)6 * n, f);
+            }
+            for (const char *link : {"arm2_7", "arm1_7"}) {
+                Eigen::Affine3d P;
+                m.getPose(link, P);
+                std::fwrite(P.m, sizeof(double), 12, f);
+            }
+            std::fwrite(q.data(), sizeof(double), n, f);
+            std::fwrite(qd.data(), sizeof(double), n, f);
+            std::fwrite(h.data(), sizeof(double), n, f);
+            std::fwrite(tau.data(), sizeof(double), n, f);
+            const int st = plugin.last_status();
+            std::fwrite(&st, sizeof(int), 1, f);
+        }
+        handle->robot().step(handle->model(), dt); // dummy-mode physics
+    }
+    const double total = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (f) std::fclose(f);
+    plugin.close();
+    std::printf("{\"config\": 0, \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, \"worst_us\": %.3f, "
+                "\"solver_errors\": %d}\n", n, ticks, total / ticks, worst, plugin.solver_errors());
+    return 0;
+}

@@ -25,3 +25,7 @@ if [ "$STEPS" = "all" ]; then
       python "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
   echo "prof rc=$?"; tail -n 5 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"
 fi
+if [ "$STEPS" = "all" ] || [ "$STEPS" = "plugin" ]; then
+  cd "$GRAFT_REPO_ROOT"
+  run dummy_driver 300 ./qppvm_amd/qppvm_dummy_driver --ticks 10000 --dump gpurun_out/dummy_dump.bin 50 || exit 1
+fi
