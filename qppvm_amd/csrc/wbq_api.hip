@@ -24,12 +24,17 @@ struct wbq_ctx {
     // batch-shared parameters (device)
     double *Kc = nullptr, *Dc = nullptr, *Kq = nullptr, *Dq = nullptr, *tmax = nullptr, *tmin = nullptr;
     int *row_sel = nullptr;
-    // owned input buffers (capacity max_batch) and the pointers the next solve reads
-    double *own[8] = {};
+    // owned inputs: one device block + one pinned host staging block, fields packed back to
+    // back for the current batch, so a host-side set_inputs is a single H2D copy
+    double *dev_in = nullptr, *host_in = nullptr;
+    hipEvent_t in_copied = nullptr;
+    bool in_pending = false;
     const double *in[8] = {};
     int batch = 0;
     bool have_inputs = false;
-    // outputs: context-owned buffers and the ones the next solve writes
+    // outputs: one device block [tau | status | iters] packed for the current batch (single
+    // D2H copy into the pinned host block), and optional caller-owned device buffers
+    double *dev_out = nullptr, *host_out = nullptr;
     double *tau = nullptr;
     int *status = nullptr;
     int *iters = nullptr;
@@ -129,9 +134,14 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
               hipMalloc(&c->Kq, n * 8) == hipSuccess && hipMalloc(&c->Dq, n * 8) == hipSuccess &&
               hipMalloc(&c->tmax, n * 8) == hipSuccess && hipMalloc(&c->tmin, n * 8) == hipSuccess &&
               hipMalloc(&c->row_sel, sizeof(int) * wbq::kM0Max) == hipSuccess;
-    for (int f = 0; ok && f < 8; ++f) ok = hipMalloc(&c->own[f], field_elems(d, f) * B * 8) == hipSuccess;
-    ok = ok && hipMalloc(&c->tau, n * B * 8) == hipSuccess && hipMalloc(&c->status, B * 4) == hipSuccess &&
-         hipMalloc(&c->iters, B * 4) == hipSuccess;
+    size_t in_elems = 0;
+    for (int f = 0; f < 8; ++f) in_elems += field_elems(d, f) * B;
+    const size_t out_bytes = n * B * 8 + 2 * B * 4 + 16;
+    ok = ok && hipMalloc(&c->dev_in, in_elems * 8) == hipSuccess &&
+         hipHostMalloc((void **)&c->host_in, in_elems * 8, hipHostMallocDefault) == hipSuccess &&
+         hipMalloc(&c->dev_out, out_bytes) == hipSuccess &&
+         hipHostMalloc((void **)&c->host_out, out_bytes, hipHostMallocDefault) == hipSuccess &&
+         hipEventCreateWithFlags(&c->in_copied, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
     ok = hipMemcpy(c->Kc, d.Kc, T6 * 8, hipMemcpyHostToDevice) == hipSuccess &&
          hipMemcpy(c->Dc, d.Dc, T6 * 8, hipMemcpyHostToDevice) == hipSuccess &&
@@ -170,20 +180,32 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
     const double *src[8] = {in->M, in->J, in->pose, in->pose_ref, in->q, in->qd, in->qref, in->h};
     for (int f = 0; f < 8; ++f)
         if (!src[f] && in->batch > 0) return fail(c, WBQ_E_INVALID, "null input pointer");
+    if (in->memory != WBQ_MEM_DEVICE && in->memory != WBQ_MEM_HOST)
+        return fail(c, WBQ_E_INVALID, "unknown memory kind");
     WBQ_HIP(hipSetDevice(c->device));
-    for (int f = 0; f < 8; ++f) {
-        if (in->memory == WBQ_MEM_DEVICE) {
-            c->in[f] = src[f];
-        } else if (in->memory == WBQ_MEM_HOST) {
-            if (in->batch > 0)
-                WBQ_HIP(hipMemcpyAsync(c->own[f], src[f], field_elems(c->d, f) * in->batch * 8,
-                                       hipMemcpyHostToDevice, c->stream));
-            c->in[f] = c->own[f];
-        } else {
-            return fail(c, WBQ_E_INVALID, "unknown memory kind");
+    if (in->memory == WBQ_MEM_DEVICE) {
+        for (int f = 0; f < 8; ++f) c->in[f] = src[f];
+    } else {
+        // the staging block may still feed the previous copy: wait for it first
+        if (c->in_pending) WBQ_HIP(hipEventSynchronize(c->in_copied));
+        size_t off = 0;
+        for (int f = 0; f < 8; ++f) {
+            const size_t e = field_elems(c->d, f) * (size_t)in->batch;
+            if (e) std::memcpy(c->host_in + off, src[f], e * 8);
+            c->in[f] = c->dev_in + off;
+            off += e;
+        }
+        if (off) {
+            WBQ_HIP(hipMemcpyAsync(c->dev_in, c->host_in, off * 8, hipMemcpyHostToDevice, c->stream));
+            WBQ_HIP(hipEventRecord(c->in_copied, c->stream));
+            c->in_pending = true;
         }
     }
     c->batch = in->batch;
+    // output block for this batch: [tau | status | iters]
+    c->tau = c->dev_out;
+    c->status = (int *)(c->dev_out + (size_t)c->batch * c->d.n);
+    c->iters = c->status + c->batch;
     c->have_inputs = true;
     return WBQ_SUCCESS;
 }
@@ -245,14 +267,22 @@ int wbq_get_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
 {
     if (!c) return WBQ_E_INVALID;
     WBQ_HIP(hipSetDevice(c->device));
-    const size_t B = (size_t)c->batch;
-    const double *dt = c->out_tau ? c->out_tau : c->tau;
-    const int *ds = c->out_status ? c->out_status : c->status;
-    const int *di = c->out_iters ? c->out_iters : c->iters;
-    if (tau && B) WBQ_HIP(hipMemcpyAsync(tau, dt, B * c->d.n * 8, hipMemcpyDeviceToHost, c->stream));
-    if (status && B) WBQ_HIP(hipMemcpyAsync(status, ds, B * 4, hipMemcpyDeviceToHost, c->stream));
-    if (iters && B) WBQ_HIP(hipMemcpyAsync(iters, di, B * 4, hipMemcpyDeviceToHost, c->stream));
+    const size_t B = (size_t)c->batch, n = (size_t)c->d.n;
+    if (B == 0) return WBQ_SUCCESS;
+    double *ht = c->host_out;
+    int *hs = (int *)(c->host_out + B * n), *hi = hs + B;
+    if (!c->out_tau && !c->out_status && !c->out_iters) {
+        // one pinned D2H copy of the packed block
+        WBQ_HIP(hipMemcpyAsync(c->host_out, c->dev_out, B * n * 8 + 2 * B * 4, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        WBQ_HIP(hipMemcpyAsync(ht, c->out_tau ? c->out_tau : c->tau, B * n * 8, hipMemcpyDeviceToHost, c->stream));
+        WBQ_HIP(hipMemcpyAsync(hs, c->out_status ? c->out_status : c->status, B * 4, hipMemcpyDeviceToHost, c->stream));
+        WBQ_HIP(hipMemcpyAsync(hi, c->out_iters ? c->out_iters : c->iters, B * 4, hipMemcpyDeviceToHost, c->stream));
+    }
     WBQ_HIP(hipStreamSynchronize(c->stream));
+    if (tau) std::memcpy(tau, ht, B * n * 8);
+    if (status) std::memcpy(status, hs, B * 4);
+    if (iters) std::memcpy(iters, hi, B * 4);
     return WBQ_SUCCESS;
 }
 
@@ -334,14 +364,13 @@ void wbq_destroy(wbq_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     for (auto &e : c->ev) (void)hipEventDestroy(e);
-    double *bufs[] = {c->Kc, c->Dc, c->Kq, c->Dq, c->tmax, c->tmin, c->tau};
+    double *bufs[] = {c->Kc, c->Dc, c->Kq, c->Dq, c->tmax, c->tmin, c->dev_in, c->dev_out};
     for (double *p : bufs)
         if (p) (void)hipFree(p);
-    for (double *p : c->own)
-        if (p) (void)hipFree(p);
+    if (c->host_in) (void)hipHostFree(c->host_in);
+    if (c->host_out) (void)hipHostFree(c->host_out);
+    if (c->in_copied) (void)hipEventDestroy(c->in_copied);
     if (c->row_sel) (void)hipFree(c->row_sel);
-    if (c->status) (void)hipFree(c->status);
-    if (c->iters) (void)hipFree(c->iters);
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->u_scr) (void)hipFree(c->u_scr);
     if (c->q1_scr) (void)hipFree(c->q1_scr);
