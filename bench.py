@@ -50,6 +50,7 @@ def main():
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from qppvm_amd.problem import QPPVMProblem
+    from qppvm_amd.shard import ShardPlan
     from qppvm_amd.synth import qppvm_instances, replicate
     from qppvm_amd.wbq import QPPVMSolver
 
@@ -59,11 +60,14 @@ def main():
         prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive
         inp = replicate(qppvm_instances(prob, 1, seed=0), B)
     else:
-        inp = qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=rank * B)
-        # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the same
-        # batch solved with the limits far away (one extra solve before timing)
+        plan = ShardPlan(B * world, world)  # weak scaling: rank r solves rows [r B, (r+1) B)
+        inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank))
+        # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the first
+        # B instances solved with the limits far away (same sample on every rank, so all ranks
+        # solve one global problem)
+        calib = inp if rank == 0 else qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=0)
         free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B, device=device)
-        tau_free, _, _ = free.solve_batch(inp)
+        tau_free, _, _ = free.solve_batch(calib)
         free.close()
         prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
     solver = QPPVMSolver(prob, max_batch=B, device=device)

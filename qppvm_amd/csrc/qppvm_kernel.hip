@@ -1,18 +1,19 @@
 // qppvm_kernel.hip -- batched QPPVM torque solve for gfx950 (MI355X), fp64.
 //
 // One QP instance per group of NP lanes (NP = 32: two instances per wave64; NP = 64: one),
-// lane i <-> joint i. A solve is two launches on one stream, nothing goes back to the host:
+// lane i <-> joint i. A solve is three launches on one stream, nothing goes back to the host:
 //
 //   qppvm_fast_kernel    every instance: stage -> task forces -> Gauss-Jordan on M ->
-//                        equality-constrained optimum -> bound check -> tau. Instances whose
-//                        optimum violates a torque bound park (u, Q1) in scratch and mark
-//                        themselves with status -1.
-//   qppvm_active_kernel  same instance -> block mapping; blocks without a marked instance exit
-//                        at once, the others run the Goldfarb-Idnani dual active set on the
-//                        torque bounds -> tau.
-//
-// The split keeps the common path lean (VGPRs, LDS, hence occupancy) and gives the iterative
-// part its own resource budget.
+//                        equality-constrained optimum -> bound check -> tau. An instance whose
+//                        optimum violates a torque bound parks (u, Q1) in scratch (status -1);
+//                        one whose level-0 rows are inconsistent (level 0 infeasible at b0)
+//                        is marked status -2.
+//   qppvm_active_kernel  status -1: Goldfarb-Idnani dual active set on the torque bounds -> tau;
+//                        an instance it finds level-0 infeasible is re-marked -2.
+//   qppvm_repair_kernel  status -2: level 0 by BVLS (y*), pins, fresh dual active set -> tau.
+// All three use the same instance -> block mapping; blocks without work exit at once.
+// Each kernel has its own register budget: the common path stays spill-free, the rare
+// ones do not weigh on it.
 //
 // The math (reference src/QPPVMPlugin.cpp:201-259):
 //   level 0  min 0.5 sum_t ||S_t J_t M^-1 x - S_t J_t M^-1 J_t^T F_t||^2      (:129-152, :177)
@@ -26,8 +27,8 @@
 // is the identity, so the dual active set needs no factorisation of H, the bound normals
 // are rows of M (given data), and the conditioning is cond(M), not cond(M)^2 as in the
 // reference's x-space H1 = M^-2. When level 0 is feasible (y* = b0, the generic case) the
-// level-0 optimality constraint A0 x = y* is exactly G u = b0; an infeasible level 0 is
-// reported as status 2.
+// level-0 optimality constraint A0 x = y* is exactly G u = b0; otherwise the repair kernel
+// computes y* and the pinned bounds first (as oracle/wbq_oracle.c:wbq_ref_qppvm_one does).
 //
 // M must be symmetric (it is read column-wise as rows).
 #include "wbq_kernels.h"
@@ -262,6 +263,119 @@ __device__ double cart_error_component(const double *P, const double *Pr, int r)
 }
 
 
+// In-place block Gauss-Jordan on an SPD matrix held one row per lane (A = row i), with NR
+// right-hand sides per row; returns true if a pivot was not positive (M not SPD). On exit
+// rhs = M^-1 rhs (row i). PN: LDS [2][NP][4] panel, RH: LDS [2][4][RHS] pivot-row rhs.
+//
+// Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing Schur
+// complement stays symmetric: pivot row k+r, column j, equals lane j's entry in column k+r.
+// Every lane publishes its BS panel entries; every lane factors the BS x BS pivot block D
+// redundantly and applies one rank-BS update:
+//   rows outside the block: row -= (a_i D^-1) P,   rows inside: row = (D^-1)_ri P,
+// so each row ends up normalised by its own pivot block (x_i = rhs_i, no division).
+// The next panel is updated and published first (lookahead), then the rest of the row.
+template <int NP, int NR, int RHS>
+__device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int n, int i, double *PN, double *RH)
+{
+    constexpr int BS = 4;
+    bool notspd = false;
+#pragma unroll
+    for (int c = 0; c < BS; ++c) PN[i * BS + c] = A[c];
+    if (i < BS) {
+#pragma unroll
+        for (int m = 0; m < NR; ++m) RH[i * RHS + m] = rhs[m];
+    }
+#pragma unroll
+    for (int kb = 0; kb < NP / BS; ++kb) {
+        const int k = kb * BS;
+        if (k < n) {
+            __syncthreads();
+            const double *pn = PN + (kb & 1) * NP * BS;
+            const double *rh = RH + (kb & 1) * BS * RHS;
+            double *pnn = PN + ((kb + 1) & 1) * NP * BS;
+            double *rhn = RH + ((kb + 1) & 1) * BS * RHS;
+            // Cholesky of the pivot block (redundant per lane)
+            double d[BS][BS];
+#pragma unroll
+            for (int r = 0; r < BS; ++r)
+#pragma unroll
+                for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
+            double il[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double dd = d[c][c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
+                notspd |= !(dd > 0.0);
+                il[c] = frsq(dd);
+#pragma unroll
+                for (int r = c + 1; r < BS; ++r) {
+                    double t = d[r][c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
+                    d[r][c] = t * il[c];
+                }
+            }
+            // solve D y = e, e = unit(i-k) for the block's own rows, else a_i = row i's panel
+            const int ri = i - k;
+            const bool inK = ri >= 0 && ri < BS;
+            double y[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double v = inK ? (ri == c ? 1.0 : 0.0) : A[k + c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
+                y[c] = v * il[c];
+            }
+#pragma unroll
+            for (int c = BS - 1; c >= 0; --c) {
+                double v = y[c];
+#pragma unroll
+                for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
+                y[c] = v * il[c];
+            }
+            const double cc = inK ? 0.0 : 1.0;
+            double hh[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) hh[c] = inK ? y[c] : -y[c];
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                double v = cc * rhs[m];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], rh[c * RHS + m], v);
+                rhs[m] = v;
+            }
+            // lookahead: next panel first
+#pragma unroll
+            for (int j = k + BS; j < k + 2 * BS && j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
+            if (k + BS < n) {
+#pragma unroll
+                for (int c = 0; c < BS; ++c)
+                    if (k + BS + c < NP) pnn[i * BS + c] = A[(k + BS + c) < NP ? k + BS + c : NP - 1];
+                const int rn = i - (k + BS);
+                if (rn >= 0 && rn < BS) {
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) rhn[rn * RHS + m] = rhs[m];
+                }
+            }
+#pragma unroll
+            for (int j = k + 2 * BS; j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
+        }
+    }
+    return notspd;
+}
+
+
 // Orthogonalise the normal held in NV against the rows of Q1T (two classical Gram-Schmidt
 // passes). Rows >= q of Q1T are finite and D1[c >= q] = 0, so every loop runs to NP
 // unguarded. Leaves d1 = Q1^T n in D1 and returns this lane's entry of z.
@@ -296,7 +410,684 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 }
 
 
+// ============================================================== level-0 repair
+// Packed lower triangle index (row-major).
+__host__ __device__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
+
+// Diagonal-pivoted Cholesky of a PSD K x K Gram held redundantly per lane (packed lower,
+// original row order; rows >= m ignored): P Gram P^T = L L^T, rank k = number of pivots
+// above tol * max diagonal. Pivoting keeps the left-over Schur diagonal at roundoff level,
+// so the rank decision is reliable (without it, a small genuine pivot inflates the
+// dependent rows' pivots far above roundoff). Static register indices throughout: the
+// dynamic pivot is applied with select chains.
+template <int K>
+struct PivChol {
+    static constexpr int T = K * (K + 1) / 2;
+    int k;           // rank
+    int piv[K];      // original row of pivot c (c < k)
+    bool used[K];    // row pivoted (or >= m)
+    double Lp[T];    // L restricted to the pivot rows, step order (packed lower)
+    double Lo[K][K]; // L row of every original row (columns = pivot steps)
+
+    __device__ static double gsym(const double (&g)[T], int i, int p)
+    {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) v = (q == p) ? g[i >= q ? tri(i, q) : tri(q, i)] : v;
+        return v;
+    }
+
+    __device__ void factor(const double (&g)[T], int m, double tol)
+    {
+        double d[K], dmx = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            d[i] = i < m ? g[tri(i, i)] : 0.0;
+            dmx = fmax(dmx, d[i]);
+            used[i] = i >= m;
+            piv[i] = 0;
+#pragma unroll
+            for (int c = 0; c < K; ++c) Lo[i][c] = 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) Lp[t] = 0.0;
+        k = 0;
+        bool stop = false;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            int p = 0;
+            double best = -1.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (!used[i] && d[i] > best) {
+                    best = d[i];
+                    p = i;
+                }
+            stop = stop || !(best > tol * dmx);
+            if (!stop) {
+                piv[c] = p;
+                k = c + 1;
+                const double lpp = sqrt(best), il = 1.0 / lpp;
+                double rp[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) v = (i == p) ? Lo[i][j] : v;
+                    rp[j] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    used[i] = used[i] || i == p;
+                    if (!used[i]) {
+                        double v = gsym(g, i, p);
+#pragma unroll
+                        for (int j = 0; j < c; ++j) v = fma(-Lo[i][j], rp[j], v);
+                        v *= il;
+                        Lo[i][c] = v;
+                        d[i] = fma(-v, v, d[i]);
+                    }
+                    if (i == p) Lo[i][c] = lpp;
+                }
+#pragma unroll
+                for (int j = 0; j < c; ++j) Lp[tri(c, j)] = rp[j];
+                Lp[tri(c, c)] = lpp;
+            }
+        }
+    }
+
+    // Weights w (original row order) of the minimum-norm least-squares solution z = A^T w of
+    // A z = r, where Gram = A A^T (rows m..K-1 absent). With C = L_D L_P^-1 relating the
+    // dependent rows D to the pivot rows P:
+    //   s = (I + C^T C)^-1 (r_P + C^T r_D),  w_P = Gram_PP^-1 s,  w_D = 0
+    // (the oracle does this solve with an SVD: oracle/wbq_oracle.c:minnorm_ls).
+    __device__ void solve(const double (&r)[K], int m, double (&w)[K]) const
+    {
+        double rh[K], H[T];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) v = (c < k && piv[c] == i) ? r[i] : v;
+            rh[c] = v;
+        }
+#pragma unroll
+        for (int p = 0; p < K; ++p)
+#pragma unroll
+            for (int q = 0; q <= p; ++q) H[tri(p, q)] = p == q ? 1.0 : 0.0;
+        double ild[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) ild[c] = c < k ? 1.0 / Lp[tri(c, c)] : 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            bool dep = i < m;
+#pragma unroll
+            for (int c = 0; c < K; ++c) dep = dep && !(c < k && piv[c] == i);
+            if (dep) {
+                double ci[K];
+#pragma unroll
+                for (int c = K - 1; c >= 0; --c) {
+                    double v = Lo[i][c];
+#pragma unroll
+                    for (int c2 = c + 1; c2 < K; ++c2) v = fma(-Lp[tri(c2, c)], ci[c2], v);
+                    ci[c] = v * ild[c];
+                }
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    rh[p] = fma(ci[p], r[i], rh[p]);
+#pragma unroll
+                    for (int q = 0; q <= p; ++q) H[tri(p, q)] = fma(ci[p], ci[q], H[tri(p, q)]);
+                }
+            }
+        }
+        double ih[K]; // Cholesky of H (SPD, well conditioned: |C| is bounded under pivoting)
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            double dd = H[tri(c, c)];
+#pragma unroll
+            for (int j = 0; j < c; ++j) dd = fma(-H[tri(c, j)], H[tri(c, j)], dd);
+            ih[c] = 1.0 / sqrt(dd);
+            H[tri(c, c)] = dd * ih[c];
+#pragma unroll
+            for (int r2 = c + 1; r2 < K; ++r2) {
+                double t = H[tri(r2, c)];
+#pragma unroll
+                for (int j = 0; j < c; ++j) t = fma(-H[tri(r2, j)], H[tri(c, j)], t);
+                H[tri(r2, c)] = t * ih[c];
+            }
+        }
+        double sv[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            double v = rh[c];
+#pragma unroll
+            for (int j = 0; j < c; ++j) v = fma(-H[tri(c, j)], sv[j], v);
+            sv[c] = v * ih[c];
+        }
+#pragma unroll
+        for (int c = K - 1; c >= 0; --c) {
+            double v = sv[c];
+#pragma unroll
+            for (int j = c + 1; j < K; ++j) v = fma(-H[tri(j, c)], sv[j], v);
+            sv[c] = v * ih[c];
+        }
+        // w_P = L_P^-T L_P^-1 s
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            double v = sv[c];
+#pragma unroll
+            for (int j = 0; j < c; ++j) v = fma(-Lp[tri(c, j)], sv[j], v);
+            sv[c] = v * ild[c];
+        }
+#pragma unroll
+        for (int c = K - 1; c >= 0; --c) {
+            double v = sv[c];
+#pragma unroll
+            for (int j = c + 1; j < K; ++j) v = fma(-Lp[tri(j, c)], sv[j], v);
+            sv[c] = v * ild[c];
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int c = 0; c < K; ++c) v = (c < k && piv[c] == i) ? sv[c] : v;
+            w[i] = v;
+        }
+    }
+
+    // Orthonormal basis of range(A^T) (lane-distributed rows): q_c = (L_P^-1 a_P)[c], c < k
+    __device__ void basis(const double (&acol)[K], double (&q)[K]) const
+    {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) v = (piv[c] == i) ? acol[i] : v;
+#pragma unroll
+            for (int j = 0; j < c; ++j) v = fma(-Lp[tri(c, j)], q[j], v);
+            q[c] = c < k ? v / Lp[tri(c, c)] : 0.0;
+        }
+    }
+};
+
+template <int NP, int K>
+__device__ __forceinline__ void isum_vec(double (&v)[K])
+{
+#pragma unroll
+    for (int m = NP / 2; m >= 1; m >>= 1)
+#pragma unroll
+        for (int c = 0; c < K; ++c) v[c] += __shfl_xor(v[c], m, NP);
+}
+
+struct RepairOut {
+    double lo, hi, u; // (possibly pinned) limits and the new u of this lane
+    int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
+};
+
+// Level-0 repair for the instances with rep set (every lane of the wave calls this; the
+// instance -> lane mapping is the kernel's). Level 0 in x-space is
+//   min 0.5 ||A0 x - b0||^2  s.t. lo <= x <= hi,   A0 = G M^-1   (QPPVMPlugin.cpp:129-152,177)
+// Solved by BVLS (Stark-Parker), the algorithm of oracle/wbq_oracle.c:wbq_ref_level0, with
+// lane i owning column a_i = (M^-1 G^T)_i (block Gauss-Jordan on the M rows, reloaded from
+// HBM/L2: this path is rare). Then y* = A0 x*, every variable the level-0 gradient
+// w = A0^T (b0 - y*) holds at a bound is pinned there (lo = hi, as wbq_ref_qppvm_one does),
+// and u is reset to the least-distance point of G u = y*, with the Q1 rows (orthonormal
+// basis of range(G^T), zero rows past its rank) in LDS for a fresh dual active set.
+// Not inlined: its registers do not weigh on the active-set loop.
+template <int NP, int M0>
+__device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff, long b, int i, bool rep, double lo,
+                                                double hi)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double *S = smem + soff;
+    constexpr int RS = NP + 1;
+    constexpr int NT = M0 * (M0 + 1) / 2;
+    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const int n = a.n, m0 = a.m0;
+    const int ic = i < n ? i : n - 1;
+    const bool row = rep && i < n;
+    RepairOut out{lo, hi, 0.0, 0, 0};
+    double gcol[M0], acol[M0], b0v[M0];
+    const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        const bool on = rep && c < m0;
+        const int rr = on ? a.row_sel[c] : 0;
+        gcol[c] = (on && row) ? a.J[(b * a.ntasks * 6 + rr) * n + ic] : 0.0;
+        b0v[c] = on ? a.b0_scr[b * kM0Max + c] : 0.0;
+        acol[c] = gcol[c];
+    }
+    // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
+    // are rebuilt below)
+    {
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, (long)a.B * n * n);
+        const int moff = (int)(8 * (b * n * n + ic));
+        double A[NP];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+#pragma unroll
+        for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+        __syncthreads();
+        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 8 * NP);
+    }
+    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)
+    double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
+    int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
+    if (row && lo == hi) {
+        st = -1;
+        xv = lo;
+    }
+    bool ex = false; // excluded from the next KKT pick (Stark-Parker anti-cycling)
+    double abm = 0.0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
+    abm = fmax(1.0, imax<NP>(fabs(abm)));
+    const double wtol = 1e-11 * abm, pintol = 1e-9 * abm;
+    int freed = -1, it = 0;
+    const int maxit = 50 * n + 100;
+    bool outer = rep;
+    while (__any(outer)) {
+        bool inner = outer;
+        while (__any(inner)) {
+            if (inner) ++it;
+            const bool fr = inner && st == 0;
+            double rv[M0], gp[NT];
+#pragma unroll
+            for (int c = 0; c < M0; ++c) rv[c] = (st == -1 || st == 1) ? acol[c] * xv : 0.0;
+#pragma unroll
+            for (int p = 0; p < M0; ++p)
+#pragma unroll
+                for (int c = 0; c <= p; ++c) gp[tri(p, c)] = fr ? acol[p] * acol[c] : 0.0;
+            isum_vec<NP, M0>(rv);
+            isum_vec<NP, NT>(gp);
+            const double kfree = isum<NP>(fr ? 1.0 : 0.0);
+#pragma unroll
+            for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
+            // minimum-norm least squares on the free set: z = A_F^T w
+            double wv[M0];
+            {
+                PivChol<M0> pc;
+                pc.factor(gp, m0, 1e-12);
+                pc.solve(rv, m0, wv);
+            }
+            double z = 0.0;
+#pragma unroll
+            for (int c = 0; c < M0; ++c) z = fma(acol[c], wv[c], z);
+            // interpolate back into the box: blocking variable = smallest step fraction < 1
+            double al = kInf;
+            if (fr) {
+                const double step = z - xv;
+                if (z < lo && step < 0.0) al = (lo - xv) / step;
+                else if (z > hi && step > 0.0) al = (hi - xv) / step;
+                if (!(al < 1.0)) al = kInf;
+            }
+            int jb = i;
+            iargmin<NP>(al, jb);
+            if (inner) {
+                if (!(kfree > 0.0)) {
+                    inner = false;
+                } else if (al >= kInf) { // z inside the box: take it
+                    if (fr) xv = z;
+                    freed = -1;
+                    inner = false;
+                } else {
+                    const double alpha = fmax(al, 0.0);
+                    if (jb == freed && alpha == 0.0) {
+                        // the variable just freed wants back through its bound: re-bind, exclude
+                        if (i == jb) {
+                            ex = true;
+                            st = (z < lo) ? -1 : 1;
+                            xv = st < 0 ? lo : hi;
+                        }
+                        inner = false;
+                    } else if (fr) {
+                        xv = fma(alpha, z - xv, xv);
+                        const double tl = 1e-14 * fmax(1.0, fabs(lo)), tu = 1e-14 * fmax(1.0, fabs(hi));
+                        if (i == jb) st = (z < lo) ? -1 : 1;
+                        else if (xv <= lo + tl && z < lo) st = -1;
+                        else if (xv >= hi - tu && z > hi) st = 1;
+                        if (st == -1) xv = lo;
+                        if (st == 1) xv = hi;
+                    }
+                    freed = -1;
+                    if (it >= maxit) inner = false;
+                }
+            }
+        }
+        // KKT on the bound variables: w = A0^T (b0 - A0 x)
+        double rf[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) rf[c] = acol[c] * xv;
+        isum_vec<NP, M0>(rf);
+        double w = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - rf[c], w);
+        double v = -kInf;
+        if (outer && (st == -1 || st == 1) && !ex && lo != hi) v = st < 0 ? w : -w;
+        int best = i;
+        iargmax<NP>(v, best);
+        if (outer) {
+            if (!(v > wtol)) {
+                outer = false;
+            } else if (it >= maxit) {
+                out.status = 1;
+                outer = false;
+            } else {
+                if (i == best) st = 0;
+                freed = best;
+                ex = false;
+            }
+        }
+    }
+    // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
+    double ys[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) ys[c] = acol[c] * xv;
+    isum_vec<NP, M0>(ys);
+    if (row) {
+        double w = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - ys[c], w);
+        if (w > pintol) out.lo = hi;       // pinned at the upper bound
+        else if (w < -pintol) out.hi = lo; // pinned at the lower bound
+    }
+    double gg[NT], rr[M0];
+#pragma unroll
+    for (int p = 0; p < M0; ++p) {
+        rr[p] = gcol[p] * uimp;
+#pragma unroll
+        for (int c = 0; c <= p; ++c) gg[tri(p, c)] = gcol[p] * gcol[c];
+    }
+    isum_vec<NP, M0>(rr);
+    isum_vec<NP, NT>(gg);
+#pragma unroll
+    for (int c = 0; c < M0; ++c) rr[c] = ys[c] - rr[c]; // y* - G u_imp (consistent)
+    double q1[M0], cv[M0];
+    {
+        PivChol<M0> pc;
+        pc.factor(gg, m0, 1e-12);
+        pc.solve(rr, m0, cv);
+        pc.basis(gcol, q1);
+    }
+    double un = uimp;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) un = fma(gcol[c], cv[c], un);
+    out.u = rep ? un : 0.0;
+    __syncthreads(); // Gauss-Jordan scratch in QA is dead
+    if (rep) {
+#pragma unroll
+        for (int c = 0; c < NP; ++c) S[L.QA + c * RS + i] = (c < M0 && c < m0) ? q1[c < M0 ? c : 0] : 0.0;
+    }
+    out.it = rep ? it : 0;
+    return out;
+}
+
+// ============================================================== active-set path
+// Goldfarb-Idnani dual active set on the torque bounds (QPPVMPlugin.cpp:203-205 limits) in
+// u-space, for the instances with go set, starting from u_i (the equality-constrained
+// optimum) with the Q1 rows in LDS (QA rows < m0, the others zero). Pinned or equal limits
+// (lo == hi) act as equalities and are never dropped. Returns this lane's x = M u; sets
+// infeasible when no step exists (then level 0 is not attainable at b0: y* != b0).
+template <int NP, int M0>
+__device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
+                                           double lo, double hi, double u_i, int &status, int &iters,
+                                           bool &infeasible)
+{
+    constexpr int RS = NP + 1;
+    constexpr bool MREG = ActiveLayout<NP>::MREG;
+    const int n = a.n, m0 = a.m0;
+    const ActiveLayout<NP> L(a.ntasks, m0);
+    const int ic = i < n ? i : n - 1;
+    const int moff = (int)(8 * (b * n * n + ic));
+    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, (long)a.B * n * n);
+    // M rows (columns, coalesced)
+    RowStore<NP, MREG> Mr;
+    Mr.bind(S + L.MA + i * RS);
+    double mrow[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+#pragma unroll
+    for (int r = 0; r < NP; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
+    if constexpr (MREG) {
+#pragma unroll
+        for (int r = 0; r < NP; ++r) Mr.v[r] = mrow[r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < NP; ++r) S[L.MA + i * RS + r] = mrow[r];
+    }
+    double nrm2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) nrm2 = fma(mrow[j], mrow[j], nrm2);
+    const double nrm = sqrt(nrm2);
+    S[L.D1 + NP + i] = 0.0;
+    S[L.U + i] = u_i;
+    RowStore<NP, MREG> Tr;
+    Tr.bind(S + L.TT + i * RS);
+    Tr.zero();
+    int k = 0, q = m0;
+    int act_p = -1, act_s = 0; // lane a < k: active inequality a (row index, sign)
+    bool act_e = false;        // lane a < k: that constraint is an equality (lo == hi)
+    double lam = 0.0;          // lane a < k: its multiplier
+    int p = 0, sg = 1;
+    double lamp = 0.0;
+    bool need_select = true;
+    const int maxit = a.max_iter;
+    const bool eqb = lo == hi;
+    infeasible = false;
+    __syncthreads();
+    while (true) {
+        const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
+        if (need_select) {
+            double v = -1.0;
+            if (row) {
+                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                const double viol = fmax(lo - s_i, s_i - hi);
+                if (viol > tol) v = viol / nrm;
+            }
+            int pi = i;
+            iargmax<NP>(v, pi);
+            if (!(v > 0.0)) go = false; // optimal
+            p = pi;
+            sg = (__shfl(lo - s_i, p, NP) > __shfl(s_i - hi, p, NP)) ? 1 : -1;
+            lamp = 0.0;
+        }
+        if (!__any(go)) break;
+        const double s_p = __shfl(s_i, p, NP);
+        const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
+        const double npn = __shfl(nrm, p, NP);
+        const bool peq = __shfl(eqb ? 1 : 0, p, NP) != 0;
+        const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
+        S[L.NV + i] = npj;
+        __syncthreads();
+        const double z = project_out<NP>(S, L, npj, q, i);
+        const double zz = isum<NP>(z * z);
+        double ra = 0.0;
+        if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
+        const double rmax = imax<NP>(fabs(ra));
+        // equality rows (pinned or lo == hi) are never dropped
+        double cand = (i < k && !act_e && ra > 1e-13 * rmax) ? lam / ra : kInf;
+        int ci = i;
+        iargmin<NP>(cand, ci);
+        const double t1 = cand;
+        const double t2 = (zz > 1e-20 * npn * npn) ? -sp / zz : kInf;
+        bool rebuild = false;
+        int cdrop = 0;
+        if (go && t1 >= kInf && t2 >= kInf) {
+            // infeasible: level 0 is not attainable at b0 inside the bounds (y* != b0)
+            infeasible = true;
+            go = false;
+        }
+        if (go) {
+            const double t = fmin(t1, t2);
+            if (i < k) lam = fma(-t, ra, lam);
+            lamp += t;
+            if (t2 < kInf) u_i = fma(t, z, u_i);
+            ++iters;
+            if (t2 <= t1) { // add p
+                const double iz = frsq(zz);
+                S[L.QA + q * RS + i] = z * iz;
+                if (i < k) Tr.set(k, -ra * iz);
+                if (i == k) {
+                    Tr.zero();
+                    Tr.set(k, iz);
+                    act_p = p;
+                    act_s = sg;
+                    act_e = peq;
+                    lam = lamp;
+                }
+                ++k;
+                ++q;
+                need_select = true;
+            } else { // drop ci (its multiplier hit zero), keep p
+                const int nap = __shfl(act_p, i + 1, NP);
+                const int nas = __shfl(act_s, i + 1, NP);
+                const bool nae = __shfl(act_e ? 1 : 0, i + 1, NP) != 0;
+                const double nlam = __shfl(lam, i + 1, NP);
+                if (i >= ci) {
+                    act_p = nap;
+                    act_s = nas;
+                    act_e = nae;
+                    lam = nlam;
+                }
+                --k;
+                cdrop = ci;
+                q = m0 + ci;
+                rebuild = true;
+                need_select = false;
+            }
+            if (iters >= maxit && go) {
+                status = 1;
+                go = false;
+            }
+        }
+        S[L.U + i] = u_i;
+        __syncthreads();
+        if (__any(rebuild)) {
+            // Re-factor the inequality directions from the dropped position on: Q1T rows
+            // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
+            if (rebuild) {
+#pragma unroll
+                for (int j = 0; j < NP; ++j)
+                    if (j >= cdrop) Tr.set(j, 0.0);
+            }
+            const int kk = rebuild ? k : 0;
+            int kmax = kk, amin = rebuild ? cdrop : NP;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                kmax = max(kmax, __shfl_xor(kmax, m, 64));
+                amin = min(amin, __shfl_xor(amin, m, 64));
+            }
+            for (int a2 = amin; a2 < kmax; ++a2) {
+                const bool on = rebuild && a2 >= cdrop && a2 < kk;
+                const int pa = __shfl(act_p, a2, NP), sa = __shfl(act_s, a2, NP);
+                const double nj = on ? sa * Mr.get(pa) : 0.0;
+                S[L.NV + i] = nj;
+                __syncthreads();
+                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
+                const double zzr = isum<NP>(zr * zr);
+                double rr2 = 0.0;
+                if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
+                if (on) {
+                    const double iz = frsq(zzr);
+                    S[L.QA + q * RS + i] = zr * iz;
+                    if (i < a2) Tr.set(a2, -rr2 * iz);
+                    if (i == a2) Tr.set(a2, iz);
+                    ++q;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    return Mr.dot(S + L.U, NP);
+}
+
+// Active-set kernel: same instance -> block mapping as the fast kernel; blocks without a
+// parked instance (status -1) exit at once. An instance whose active set finds level 0
+// infeasible is handed on to the repair kernel with status -2.
+template <int NP, int M0>
+__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
+{
+    constexpr int IPW = kWave / NP;
+    constexpr int RS = NP + 1;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const int sub = threadIdx.x / NP;
+    const int i = threadIdx.x - sub * NP;
+    double *S = smem + sub * L.SIZE;
+    const long b0_ = (long)blockIdx.x * IPW + sub;
+    const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
+    if (!__any(valid)) return;
+    WBQ_STAMP(4);
+    const long b = valid ? b0_ : 0;
+    const int n = a.n;
+    const bool row = valid && i < n;
+    const double h_i = row ? a.h[b * n + i] : 0.0;
+    const double lo = row ? a.tau_min[i] - h_i : -kInf;
+    const double hi = row ? a.tau_max[i] - h_i : kInf;
+    const double *qs = a.q1_scr + b * kM0Max * NP;
+#pragma unroll
+    for (int c = 0; c < NP; ++c)
+        S[L.QA + c * RS + i] = (valid && c < M0 && c < a.m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
+    int status = 0, iters = 0;
+    bool infeasible = false;
+    WBQ_STAMP(6);
+    const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0, status,
+                                        iters, infeasible);
+    if (infeasible) {
+        if (valid && i == 0) a.status[b] = -2; // level-0 repair kernel
+    } else {
+        double tau_i = x_i + h_i;
+        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+        if (row) a.tau[b * n + i] = tau_i;
+        if (valid && i == 0) {
+            a.status[b] = status;
+            a.iters[b] = iters;
+        }
+    }
+    WBQ_STAMP(7);
+}
+
+// Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by the
+// active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. Rare path:
+// kept out of the other kernels so that its registers do not weigh on them.
+template <int NP, int M0>
+__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(const QppvmArgs a)
+{
+    constexpr int IPW = kWave / NP;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const int sub = threadIdx.x / NP;
+    const int i = threadIdx.x - sub * NP;
+    double *S = smem + sub * L.SIZE;
+    const long b0_ = (long)blockIdx.x * IPW + sub;
+    const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -2;
+    if (!__any(valid)) return;
+    const long b = valid ? b0_ : 0;
+    const int n = a.n;
+    const bool row = valid && i < n;
+    const double h_i = row ? a.h[b * n + i] : 0.0;
+    const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid, row ? a.tau_min[i] - h_i : -kInf,
+                                               row ? a.tau_max[i] - h_i : kInf);
+    int status = ro.status, iters = 0;
+    bool infeasible = false;
+    const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status, iters,
+                                        infeasible);
+    if (infeasible && status == 0) status = 2;
+    double tau_i = x_i + h_i;
+    if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+    if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+    if (row) a.tau[b * n + i] = tau_i;
+    if (valid && i == 0) {
+        a.status[b] = status;
+        a.iters[b] = iters + ro.it;
+    }
+}
+
 // ====================================================================== fast path
+// An instance whose equality-constrained optimum violates a bound parks (u, Q1) in scratch
+// for qppvm_active_kernel (status -1); one whose level 0 is infeasible at b0 goes to
+// qppvm_repair_kernel (status -2).
 template <int NP, int M0>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
 {
@@ -396,111 +1187,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
         rhs[1 + t] = c; // J_t^T F_t
     }
-    // Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing
-    // Schur complement stays symmetric: pivot row k+r, column j, equals lane j's entry in
-    // column k+r. Every lane publishes its BS panel entries; every lane factors the BS x BS
-    // pivot block D redundantly and applies one rank-BS update:
-    //   rows outside the block: row -= (a_i D^-1) P,   rows inside: row = (D^-1)_ri P,
-    // so each row ends up normalised by its own pivot block (x_i = rhs_i, no division).
-    // The next panel is updated and published first (lookahead), then the rest of the row.
-    constexpr int BS = FastLayout<NP>::BS;
-    bool notspd = false;
-    {
-        double *pn0 = S + L.PN;
-#pragma unroll
-        for (int c = 0; c < BS; ++c) pn0[i * BS + c] = A[c];
-        if (i < BS) {
-#pragma unroll
-            for (int m = 0; m < 1 + kTMax; ++m) S[L.RH + i * 8 + m] = rhs[m];
-        }
-    }
-#pragma unroll
-    for (int kb = 0; kb < NP / BS; ++kb) {
-        const int k = kb * BS;
-        if (k < n) {
-            __syncthreads();
-            const double *pn = S + L.PN + (kb & 1) * NP * BS;
-            const double *rh = S + L.RH + (kb & 1) * BS * 8;
-            double *pnn = S + L.PN + ((kb + 1) & 1) * NP * BS;
-            double *rhn = S + L.RH + ((kb + 1) & 1) * BS * 8;
-            // Cholesky of the pivot block (redundant per lane)
-            double d[BS][BS];
-#pragma unroll
-            for (int r = 0; r < BS; ++r)
-#pragma unroll
-                for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
-            double il[BS];
-#pragma unroll
-            for (int c = 0; c < BS; ++c) {
-                double dd = d[c][c];
-#pragma unroll
-                for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
-                notspd |= !(dd > 0.0);
-                il[c] = frsq(dd);
-#pragma unroll
-                for (int r = c + 1; r < BS; ++r) {
-                    double t = d[r][c];
-#pragma unroll
-                    for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
-                    d[r][c] = t * il[c];
-                }
-            }
-            // solve D y = e, e = unit(i-k) for the block's own rows, else a_i = row i's panel
-            const int ri = i - k;
-            const bool inK = ri >= 0 && ri < BS;
-            double y[BS];
-#pragma unroll
-            for (int c = 0; c < BS; ++c) {
-                double v = inK ? (ri == c ? 1.0 : 0.0) : A[k + c];
-#pragma unroll
-                for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
-                y[c] = v * il[c];
-            }
-#pragma unroll
-            for (int c = BS - 1; c >= 0; --c) {
-                double v = y[c];
-#pragma unroll
-                for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
-                y[c] = v * il[c];
-            }
-            const double cc = inK ? 0.0 : 1.0;
-            double hh[BS];
-#pragma unroll
-            for (int c = 0; c < BS; ++c) hh[c] = inK ? y[c] : -y[c];
-#pragma unroll
-            for (int m = 0; m < 1 + kTMax; ++m) {
-                double v = cc * rhs[m];
-#pragma unroll
-                for (int c = 0; c < BS; ++c) v = fma(hh[c], rh[c * 8 + m], v);
-                rhs[m] = v;
-            }
-            // lookahead: next panel first
-#pragma unroll
-            for (int j = k + BS; j < k + 2 * BS && j < NP; ++j) {
-                double v = cc * A[j];
-#pragma unroll
-                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
-                A[j] = v;
-            }
-            if (k + BS < n) {
-#pragma unroll
-                for (int c = 0; c < BS; ++c)
-                    if (k + BS + c < NP) pnn[i * BS + c] = A[(k + BS + c) < NP ? k + BS + c : NP - 1];
-                const int rn = i - (k + BS);
-                if (rn >= 0 && rn < BS) {
-#pragma unroll
-                    for (int m = 0; m < 1 + kTMax; ++m) rhn[rn * 8 + m] = rhs[m];
-                }
-            }
-#pragma unroll
-            for (int j = k + 2 * BS; j < NP; ++j) {
-                double v = cc * A[j];
-#pragma unroll
-                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
-                A[j] = v;
-            }
-        }
-    }
+    bool notspd = block_gj<NP, 1 + kTMax, 8>(A, rhs, n, i, S + L.PN, S + L.RH);
     const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
 #pragma unroll
     for (int t = 0; t < kTMax; ++t)
@@ -607,7 +1294,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     int status = 0;
     if (a.limits_crossed) status = 2; // tau_min > tau_max somewhere: infeasible everywhere
     if (notspd) status = 3;           // (instance-uniform: pivots are broadcast values)
-    if (status == 0 && eqres > 1e-9 * rmx) status = 2; // level 0 infeasible
+    // rows dropped as dependent are not met: y* != b0, level 0 itself is infeasible at b0 and
+    // the active-set kernel runs the level-0 repair (BVLS for y*) first
+    const bool l0bad = status == 0 && eqres > 1e-9 * rmx;
     double flag = 0.0;
     if (row) {
         const double tol = 1e-10 * fmax(1.0, fmax(fabs(x_i), fmax(fabs(lo), fabs(hi))));
@@ -616,7 +1305,18 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     }
     flag = imax<NP>(flag);
     if (flag >= 2.0 && status == 0) status = 3;
-    const bool active = flag > 0.0 && status == 0 && valid;
+    const bool active = (flag > 0.0 || l0bad) && status == 0 && valid;
+    if (__any(active)) { // b0 = res + G u_imp for the level-0 repair
+        S[L.U + i] = u_imp;
+        __syncthreads();
+        if (active && i < m0) {
+            const int rr = a.row_sel[i];
+            double v = S[L.RES + i];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) v = fma(S[L.JR + rr * NP + j], S[L.U + j], v);
+            a.b0_scr[b * kM0Max + i] = v;
+        }
+    }
 
     if (!active) {
         double tau_i = x_i + h_i;
@@ -626,8 +1326,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             a.status[b] = status;
             a.iters[b] = 0;
         }
-    } else {
-        // park (u, Q1) for the active-set kernel; Q1 = G^T L^-T row by row
+    }
+    if (__any(active)) {
+        // Q1 = G^T L^-T row by row
         double q1[M0];
 #pragma unroll
         for (int c = 0; c < M0; ++c) {
@@ -636,218 +1337,18 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], q1[k], v);
             q1[c] = v * il[c];
         }
-        double *us = a.u_scr + b * NP;
-        double *qs = a.q1_scr + b * kM0Max * NP;
-        us[i] = u_i;
+        if (active) a.ui_scr[b * NP + i] = u_imp; // for the level-0 repair
+        if (active) { // park (u, Q1) for the active-set kernel
+            double *us = a.u_scr + b * NP;
+            double *qs = a.q1_scr + b * kM0Max * NP;
+            us[i] = u_i;
 #pragma unroll
-        for (int c = 0; c < M0; ++c)
-            if (c < m0) qs[c * NP + i] = q1[c];
-        if (i == 0) a.status[b] = -1; // picked up by the active-set kernel
+            for (int c = 0; c < M0; ++c)
+                if (c < m0) qs[c * NP + i] = q1[c];
+            if (i == 0) a.status[b] = l0bad ? -2 : -1; // picked up by the active-set kernel
+        }
     }
     WBQ_STAMP(5);
-}
-
-// ============================================================== active-set path
-template <int NP, int M0>
-__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
-{
-    constexpr int IPW = kWave / NP;
-    constexpr int RS = NP + 1;
-    constexpr bool MREG = ActiveLayout<NP>::MREG;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int n = a.n, m0 = a.m0;
-    const ActiveLayout<NP> L(a.ntasks, m0);
-    const int tid = threadIdx.x;
-    const int sub = tid / NP;
-    const int i = tid - sub * NP;
-    double *S = smem + sub * L.SIZE;
-    const long Bn = (long)a.B * n;
-    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-    const int ic = i < n ? i : n - 1;
-    {
-        const long b0_ = (long)blockIdx.x * IPW + sub;
-        // instances the fast kernel parked (status -1); blocks with none exit at once
-        const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
-        if (!__any(valid)) return;
-        WBQ_STAMP(4);
-        const long b = valid ? b0_ : 0;
-        const bool row = valid && i < n;
-        const long bn = b * n;
-        const int moff = (int)(8 * (b * n * n + ic));
-        // M rows (columns, coalesced), h, limits, u and Q1 from the fast kernel
-        RowStore<NP, MREG> Mr;
-        Mr.bind(S + L.MA + i * RS);
-        double mrow[NP];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
-#pragma unroll
-        for (int r = 0; r < NP; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
-        if constexpr (MREG) {
-#pragma unroll
-            for (int r = 0; r < NP; ++r) Mr.v[r] = mrow[r];
-        } else {
-#pragma unroll
-            for (int r = 0; r < NP; ++r) S[L.MA + i * RS + r] = mrow[r];
-        }
-        const double h_i = row ? a.h[bn + i] : 0.0;
-        const double lo = row ? a.tau_min[i] - h_i : -kInf;
-        const double hi = row ? a.tau_max[i] - h_i : kInf;
-        double u_i = valid ? a.u_scr[b * NP + i] : 0.0;
-        const double *qs = a.q1_scr + b * kM0Max * NP;
-#pragma unroll
-        for (int c = 0; c < NP; ++c)
-            S[L.QA + c * RS + i] = (valid && c < M0 && c < m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
-        S[L.D1 + NP + i] = 0.0;
-        S[L.U + i] = u_i;
-        RowStore<NP, MREG> Tr;
-        Tr.bind(S + L.TT + i * RS);
-        Tr.zero();
-        double nrm2 = 0.0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) nrm2 = fma(mrow[j], mrow[j], nrm2);
-        const double nrm = sqrt(nrm2);
-        __syncthreads();
-
-        int status = 0;
-        bool go = valid;
-        int k = 0, q = m0, iters = 0;
-        int act_p = -1, act_s = 0; // lane a < k: active inequality a (row index, sign)
-        double lam = 0.0;          // lane a < k: its multiplier
-        int p = 0, sg = 1;
-        double lamp = 0.0;
-        bool need_select = true;
-        const int maxit = a.max_iter;
-        WBQ_STAMP(6);
-
-        while (true) {
-            const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
-            if (need_select) {
-                double v = -1.0;
-                if (row) {
-                    const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
-                    const double viol = fmax(lo - s_i, s_i - hi);
-                    if (viol > tol) v = viol / nrm;
-                }
-                int pi = i;
-                iargmax<NP>(v, pi);
-                if (!(v > 0.0)) go = false; // optimal
-                p = pi;
-                sg = (__shfl(lo - s_i, p, NP) > __shfl(s_i - hi, p, NP)) ? 1 : -1;
-                lamp = 0.0;
-            }
-            if (!__any(go)) break;
-            const double s_p = __shfl(s_i, p, NP);
-            const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
-            const double npn = __shfl(nrm, p, NP);
-            const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
-            S[L.NV + i] = npj;
-            __syncthreads();
-            const double z = project_out<NP>(S, L, npj, q, i);
-            const double zz = isum<NP>(z * z);
-            double ra = 0.0;
-            if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
-            const double rmax = imax<NP>(fabs(ra));
-            double cand = (i < k && ra > 1e-13 * rmax) ? lam / ra : kInf;
-            int ci = i;
-            iargmin<NP>(cand, ci);
-            const double t1 = cand;
-            const double t2 = (zz > 1e-20 * npn * npn) ? -sp / zz : kInf;
-            bool rebuild = false;
-            int cdrop = 0;
-            if (go && t1 >= kInf && t2 >= kInf) {
-                status = 2; // infeasible
-                go = false;
-            }
-            if (go) {
-                const double t = fmin(t1, t2);
-                if (i < k) lam = fma(-t, ra, lam);
-                lamp += t;
-                if (t2 < kInf) u_i = fma(t, z, u_i);
-                ++iters;
-                if (t2 <= t1) { // add p
-                    const double iz = frsq(zz);
-                    S[L.QA + q * RS + i] = z * iz;
-                    if (i < k) Tr.set(k, -ra * iz);
-                    if (i == k) {
-                        Tr.zero();
-                        Tr.set(k, iz);
-                        act_p = p;
-                        act_s = sg;
-                        lam = lamp;
-                    }
-                    ++k;
-                    ++q;
-                    need_select = true;
-                } else { // drop ci (its multiplier hit zero), keep p
-                    const int nap = __shfl(act_p, i + 1, NP);
-                    const int nas = __shfl(act_s, i + 1, NP);
-                    const double nlam = __shfl(lam, i + 1, NP);
-                    if (i >= ci) {
-                        act_p = nap;
-                        act_s = nas;
-                        lam = nlam;
-                    }
-                    --k;
-                    cdrop = ci;
-                    q = m0 + ci;
-                    rebuild = true;
-                    need_select = false;
-                }
-                if (iters >= maxit && go) {
-                    status = 1;
-                    go = false;
-                }
-            }
-            S[L.U + i] = u_i;
-            __syncthreads();
-            if (__any(rebuild)) {
-                // Re-factor the inequality directions from the dropped position on: Q1T rows
-                // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
-                if (rebuild) {
-#pragma unroll
-                    for (int j = 0; j < NP; ++j)
-                        if (j >= cdrop) Tr.set(j, 0.0);
-                }
-                const int kk = rebuild ? k : 0;
-                int kmax = kk, amin = rebuild ? cdrop : NP;
-#pragma unroll
-                for (int m = 32; m >= 1; m >>= 1) {
-                    kmax = max(kmax, __shfl_xor(kmax, m, 64));
-                    amin = min(amin, __shfl_xor(amin, m, 64));
-                }
-                for (int a2 = amin; a2 < kmax; ++a2) {
-                    const bool on = rebuild && a2 >= cdrop && a2 < kk;
-                    const int pa = __shfl(act_p, a2, NP), sa = __shfl(act_s, a2, NP);
-                    const double nj = on ? sa * Mr.get(pa) : 0.0;
-                    S[L.NV + i] = nj;
-                    __syncthreads();
-                    const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
-                    const double zzr = isum<NP>(zr * zr);
-                    double rr2 = 0.0;
-                    if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
-                    if (on) {
-                        const double iz = frsq(zzr);
-                        S[L.QA + q * RS + i] = zr * iz;
-                        if (i < a2) Tr.set(a2, -rr2 * iz);
-                        if (i == a2) Tr.set(a2, iz);
-                        ++q;
-                    }
-                    __syncthreads();
-                }
-            }
-        }
-
-        const double x_i = Mr.dot(S + L.U, NP);
-        double tau_i = x_i + h_i;
-        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
-        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
-        if (row) a.tau[bn + i] = tau_i;
-        if (valid && i == 0) {
-            a.status[b] = status;
-            a.iters[b] = iters;
-        }
-        WBQ_STAMP(7);
-    }
 }
 
 template <int NP, typename Lay, typename K>
@@ -868,12 +1369,14 @@ template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
 {
     constexpr int IPW = kWave / NP;
-    static size_t attr_fast = 0, attr_active = 0;
+    static size_t attr_fast = 0, attr_active = 0, attr_repair = 0;
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
     hipError_t e = launch_one<NP, FastLayout<NP>>(qppvm_fast_kernel<NP, M0>, a, grid, stream, attr_fast);
     if (e != hipSuccess) return e;
-    return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
+    e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
+    if (e != hipSuccess) return e;
+    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, grid, stream, attr_repair);
 }
 
 }  // namespace

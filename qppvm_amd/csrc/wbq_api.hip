@@ -50,6 +50,7 @@ struct wbq_ctx {
     std::string err;
     unsigned long long *stamps = nullptr; // diagnostic builds only
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
+    double *ui_scr = nullptr, *b0_scr = nullptr; // u_imp and b0 for the level-0 repair
 };
 
 namespace {
@@ -154,7 +155,9 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     {
         const size_t np = (size_t)wbq::lanes_per_instance(d.n);
         ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
-             hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess;
+             hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
+             hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
+             hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess;
         if (!ok) return cleanup(WBQ_E_DEVICE);
     }
 #ifdef WBQ_STAMPS
@@ -244,6 +247,8 @@ int wbq_solve(wbq_ctx *c)
     a.stamps = c->stamps;
     a.u_scr = c->u_scr;
     a.q1_scr = c->q1_scr;
+    a.ui_scr = c->ui_scr;
+    a.b0_scr = c->b0_scr;
 
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
@@ -374,6 +379,8 @@ void wbq_destroy(wbq_ctx *c)
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->u_scr) (void)hipFree(c->u_scr);
     if (c->q1_scr) (void)hipFree(c->q1_scr);
+    if (c->ui_scr) (void)hipFree(c->ui_scr);
+    if (c->b0_scr) (void)hipFree(c->b0_scr);
 
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;

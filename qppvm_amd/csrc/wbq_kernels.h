@@ -28,9 +28,12 @@ struct QppvmArgs {
     int *iters;      // [B]
     unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [grid][kStamps] s_memtime
     // fast kernel -> active-set kernel hand-off (device scratch sized for max_batch); the
-    // fast kernel marks an instance that needs active-set steps with status -1
-    double *u_scr;   // [B][NP]
-    double *q1_scr;  // [B][kM0Max][NP]
+    // fast kernel marks an instance that needs active-set steps with status -1, one whose
+    // level-0 rows are inconsistent (level 0 needs the BVLS repair) with status -2
+    double *u_scr;   // [B][NP]   u at the equality-constrained optimum
+    double *q1_scr;  // [B][kM0Max][NP]  Q1 = G^T L^-T
+    double *ui_scr;  // [B][NP]   u_imp = M^-1 tau_imp
+    double *b0_scr;  // [B][kM0Max]  b0 = G w_t (level-0 targets)
 };
 
 constexpr int kStamps = 8;
