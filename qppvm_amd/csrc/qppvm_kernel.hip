@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
+    if (a.work[a.epoch * 2] == 0) return; // nothing parked in this solve
     const long b0_ = (long)blockIdx.x * IPW + sub;
     const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
     if (!__any(valid)) return;
@@ -1034,7 +1035,10 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0, status,
                                         iters, infeasible);
     if (infeasible) {
-        if (valid && i == 0) a.status[b] = -2; // level-0 repair kernel
+        if (valid && i == 0) {
+            a.status[b] = -2; // level-0 repair kernel
+            a.work[a.epoch * 2 + 1] = 1;
+        }
     } else {
         double tau_i = x_i + h_i;
         if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
@@ -1060,6 +1064,11 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's flags (its parity was last used
+        a.work[(a.epoch ^ 1) * 2] = 0;         // by the previous solve, which has completed)
+        a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+    }
+    if (a.work[a.epoch * 2 + 1] == 0) return; // no level-0 repair in this solve
     const long b0_ = (long)blockIdx.x * IPW + sub;
     const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -2;
     if (!__any(valid)) return;
@@ -1345,7 +1354,10 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 #pragma unroll
             for (int c = 0; c < M0; ++c)
                 if (c < m0) qs[c * NP + i] = q1[c];
-            if (i == 0) a.status[b] = l0bad ? -2 : -1; // picked up by the active-set kernel
+            if (i == 0) {
+                a.status[b] = l0bad ? -2 : -1; // picked up by the active-set / repair kernel
+                a.work[a.epoch * 2 + (l0bad ? 1 : 0)] = 1;
+            }
         }
     }
     WBQ_STAMP(5);

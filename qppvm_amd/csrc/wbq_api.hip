@@ -51,6 +51,8 @@ struct wbq_ctx {
     unsigned long long *stamps = nullptr; // diagnostic builds only
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
     double *ui_scr = nullptr, *b0_scr = nullptr; // u_imp and b0 for the level-0 repair
+    int *work = nullptr; // [2][2] per-solve work flags (see wbq_kernels.h)
+    int epoch = 0;
 };
 
 namespace {
@@ -157,7 +159,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
         ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
-             hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess;
+             hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess &&
+             hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess;
         if (!ok) return cleanup(WBQ_E_DEVICE);
     }
 #ifdef WBQ_STAMPS
@@ -249,11 +252,14 @@ int wbq_solve(wbq_ctx *c)
     a.q1_scr = c->q1_scr;
     a.ui_scr = c->ui_scr;
     a.b0_scr = c->b0_scr;
+    a.work = c->work;
+    a.epoch = c->epoch;
 
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
     WBQ_HIP(wbq::launch_qppvm(a, c->stream));
+    if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
     if (timed) {
         WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
         c->ev_used += 2;
@@ -381,6 +387,7 @@ void wbq_destroy(wbq_ctx *c)
     if (c->q1_scr) (void)hipFree(c->q1_scr);
     if (c->ui_scr) (void)hipFree(c->ui_scr);
     if (c->b0_scr) (void)hipFree(c->b0_scr);
+    if (c->work) (void)hipFree(c->work);
 
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;

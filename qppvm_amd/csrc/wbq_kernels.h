@@ -34,6 +34,12 @@ struct QppvmArgs {
     double *q1_scr;  // [B][kM0Max][NP]  Q1 = G^T L^-T
     double *ui_scr;  // [B][NP]   u_imp = M^-1 tau_imp
     double *b0_scr;  // [B][kM0Max]  b0 = G w_t (level-0 targets)
+    // per-solve work flags, double-buffered by solve parity: work[epoch*2 + 0] = some instance
+    // parked for the active-set kernel, [+1] = some for the repair kernel. A follow-up
+    // kernel with no work exits on one broadcast load; the repair kernel (the last launch)
+    // clears the other parity's flags for the next solve.
+    int *work;       // [2][2]
+    int epoch;       // 0 / 1
 };
 
 constexpr int kStamps = 8;
