@@ -419,6 +419,7 @@ int wbq_ref_level0(int m, int n, const double *A, const double *b, const double 
             if (jblk < 0) {
                 for (int c = 0; c < k; ++c) x[F[c]] = z[c];
                 freed = -1;
+                for (int i = 0; i < n; ++i) excl[i] = 0; /* progress: exclusions expire */
                 break;
             }
             if (alpha < 0.0) alpha = 0.0;
@@ -432,6 +433,7 @@ int wbq_ref_level0(int m, int n, const double *A, const double *b, const double 
                 freed = -1;
                 break;
             }
+            for (int i = 0; i < n; ++i) excl[i] = 0; /* progress: exclusions expire */
             for (int c = 0; c < k; ++c) {
                 const int i = F[c];
                 x[i] += alpha * (z[c] - x[i]);
@@ -470,9 +472,8 @@ int wbq_ref_level0(int m, int n, const double *A, const double *b, const double 
             status = WBQ_REF_OK;
             break;
         }
-        state[best] = 0;
+        state[best] = 0; /* exclusions persist until the inner loop makes progress */
         freed = best;
-        for (int i = 0; i < n; ++i) excl[i] = 0;
     }
 out:
     if (iters) *iters = it;

@@ -1,7 +1,8 @@
 // qppvm_kernel.hip -- batched QPPVM torque solve for gfx950 (MI355X), fp64.
 //
 // One QP instance per group of NP lanes (NP = 32: two instances per wave64; NP = 64: one),
-// lane i <-> joint i. A solve is three launches on one stream, nothing goes back to the host:
+// lane i <-> joint i. A solve is two (NP = 32) or three launches on one stream, nothing goes back
+// to the host:
 //
 //   qppvm_fast_kernel    every instance: stage -> task forces -> Gauss-Jordan on M ->
 //                        equality-constrained optimum -> bound check -> tau. An instance whose
@@ -9,7 +10,9 @@
 //                        one whose level-0 rows are inconsistent (level 0 infeasible at b0)
 //                        is marked status -2.
 //   qppvm_active_kernel  status -1: Goldfarb-Idnani dual active set on the torque bounds -> tau;
-//                        an instance it finds level-0 infeasible is re-marked -2.
+//                        an instance it finds level-0 infeasible is re-marked -2. For NP = 32
+//                        this runs inline at the end of the fast kernel instead (its LDS
+//                        layout fits in the same budget), saving a launch.
 //   qppvm_repair_kernel  status -2: level 0 by BVLS (y*), pins, fresh dual active set -> tau.
 // All three use the same instance -> block mapping; blocks without work exit at once.
 // Each kernel has its own register budget: the common path stays spill-free, the rare
@@ -92,6 +95,17 @@ struct ActiveLayout {
         NV = D1B + NP;                    // n_p
         BC = NV + NP;                     // broadcast scratch
         SIZE = (BC + NP + 1) & ~1;
+    }
+};
+
+// Per-instance LDS of the fast kernel: with MERGED the active-set layout reuses it afterwards
+template <int NP, bool MERGED>
+struct FastLdsLayout {
+    int SIZE;
+    __host__ __device__ FastLdsLayout(int T, int m0)
+    {
+        const int f = FastLayout<NP>(T, m0).SIZE, g = ActiveLayout<NP>(T, m0).SIZE;
+        SIZE = (MERGED && g > f) ? g : f;
     }
 };
 
@@ -622,6 +636,7 @@ __device__ __forceinline__ void isum_vec(double (&v)[K])
 struct RepairOut {
     double lo, hi, u; // (possibly pinned) limits and the new u of this lane
     int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
+    bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
 };
 
 // Level-0 repair for the instances with rep set (every lane of the wave calls this; the
@@ -636,7 +651,7 @@ struct RepairOut {
 // Not inlined: its registers do not weigh on the active-set loop.
 template <int NP, int M0>
 __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff, long b, int i, bool rep, double lo,
-                                                double hi)
+                                                double hi, bool warm)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double *S = smem + soff;
@@ -646,7 +661,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     const int n = a.n, m0 = a.m0;
     const int ic = i < n ? i : n - 1;
     const bool row = rep && i < n;
-    RepairOut out{lo, hi, 0.0, 0, 0};
+    RepairOut out{lo, hi, 0.0, 0, 0, false};
     double gcol[M0], acol[M0], b0v[M0];
     const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
 #pragma unroll
@@ -673,6 +688,11 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)
     double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
     int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
+    if (row && warm) {    // warm start: the bound state of the last repair (any state is valid)
+        const int w = a.ws_state[b * NP + i];
+        st = (w < 0) ? -1 : (w > 0 ? 1 : 0);
+        xv = st < 0 ? lo : (st > 0 ? hi : xv);
+    }
     if (row && lo == hi) {
         st = -1;
         xv = lo;
@@ -681,8 +701,9 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     double abm = 0.0;
 #pragma unroll
     for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
-    abm = fmax(1.0, imax<NP>(fabs(abm)));
-    const double wtol = 1e-11 * abm, pintol = 1e-9 * abm;
+    const double wtb = fabs(abm);
+    abm = fmax(1.0, imax<NP>(wtb));
+    const double pintol = 1e-9 * abm;
     int freed = -1, it = 0;
     const int maxit = 50 * n + 100;
     bool outer = rep;
@@ -729,6 +750,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
                 } else if (al >= kInf) { // z inside the box: take it
                     if (fr) xv = z;
                     freed = -1;
+                    ex = false; // progress: exclusions expire
                     inner = false;
                 } else {
                     const double alpha = fmax(al, 0.0);
@@ -740,14 +762,17 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
                             xv = st < 0 ? lo : hi;
                         }
                         inner = false;
-                    } else if (fr) {
-                        xv = fma(alpha, z - xv, xv);
-                        const double tl = 1e-14 * fmax(1.0, fabs(lo)), tu = 1e-14 * fmax(1.0, fabs(hi));
-                        if (i == jb) st = (z < lo) ? -1 : 1;
-                        else if (xv <= lo + tl && z < lo) st = -1;
-                        else if (xv >= hi - tu && z > hi) st = 1;
-                        if (st == -1) xv = lo;
-                        if (st == 1) xv = hi;
+                    } else {
+                        ex = false; // progress: exclusions expire
+                        if (fr) {
+                            xv = fma(alpha, z - xv, xv);
+                            const double tl = 1e-14 * fmax(1.0, fabs(lo)), tu = 1e-14 * fmax(1.0, fabs(hi));
+                            if (i == jb) st = (z < lo) ? -1 : 1;
+                            else if (xv <= lo + tl && z < lo) st = -1;
+                            else if (xv >= hi - tu && z > hi) st = 1;
+                            if (st == -1) xv = lo;
+                            if (st == 1) xv = hi;
+                        }
                     }
                     freed = -1;
                     if (it >= maxit) inner = false;
@@ -759,9 +784,15 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
 #pragma unroll
         for (int c = 0; c < M0; ++c) rf[c] = acol[c] * xv;
         isum_vec<NP, M0>(rf);
-        double w = 0.0;
+        double w = 0.0, wx = 0.0;
 #pragma unroll
-        for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - rf[c], w);
+        for (int c = 0; c < M0; ++c) {
+            w = fma(acol[c], b0v[c] - rf[c], w);
+            wx = fma(acol[c], rf[c], wx);
+        }
+        // KKT tolerance relative to the terms of w = A0^T b0 - A0^T A0 x (with b0 ~ 0 the
+        // second dominates, and its roundoff must not read as a descent direction)
+        const double wtol = 1e-11 * fmax(abm, imax<NP>(fmax(wtb, fabs(wx))));
         double v = -kInf;
         if (outer && (st == -1 || st == 1) && !ex && lo != hi) v = st < 0 ? w : -w;
         int best = i;
@@ -773,17 +804,26 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
                 out.status = 1;
                 outer = false;
             } else {
-                if (i == best) st = 0;
+                if (i == best) st = 0; // exclusions persist until the inner loop makes progress
                 freed = best;
-                ex = false;
             }
         }
     }
     // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
+    if (row) a.ws_state[b * NP + i] = (signed char)(st == 2 ? 0 : st);
     double ys[M0];
 #pragma unroll
     for (int c = 0; c < M0; ++c) ys[c] = acol[c] * xv;
     isum_vec<NP, M0>(ys);
+    {
+        double gap = 0.0, bmx = 1.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            gap = fmax(gap, fabs(ys[c] - b0v[c]));
+            bmx = fmax(bmx, fabs(b0v[c]));
+        }
+        out.l0inf = rep && gap > 1e-9 * bmx;
+    }
     if (row) {
         double w = 0.0;
 #pragma unroll
@@ -1076,8 +1116,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
     const int n = a.n;
     const bool row = valid && i < n;
     const double h_i = row ? a.h[b * n + i] : 0.0;
+    const bool warm = valid && a.ws_hint[b] != 0;
     const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid, row ? a.tau_min[i] - h_i : -kInf,
-                                               row ? a.tau_max[i] - h_i : kInf);
+                                               row ? a.tau_max[i] - h_i : kInf, warm);
     int status = ro.status, iters = 0;
     bool infeasible = false;
     const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status, iters,
@@ -1090,14 +1131,16 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
     if (valid && i == 0) {
         a.status[b] = status;
         a.iters[b] = iters + ro.it;
+        a.ws_hint[b] = ro.l0inf ? 1 : 0;
     }
 }
 
 // ====================================================================== fast path
-// An instance whose equality-constrained optimum violates a bound parks (u, Q1) in scratch
-// for qppvm_active_kernel (status -1); one whose level 0 is infeasible at b0 goes to
-// qppvm_repair_kernel (status -2).
-template <int NP, int M0>
+// An instance whose equality-constrained optimum violates a bound needs the dual active
+// set: with MERGED (NP = 32, where the active-set layout fits next to the fast one) it runs
+// right here, inline; otherwise it parks (u, Q1) in scratch for qppvm_active_kernel
+// (status -1). One whose level 0 is infeasible at b0 goes to qppvm_repair_kernel (-2).
+template <int NP, int M0, bool MERGED>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -1109,7 +1152,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const int i = tid - sub * NP;
     const long b = (long)blockIdx.x * IPW + sub;
     const bool valid = b < a.B;
-    double *S = smem + sub * L.SIZE;
+    double *S = smem + sub * FastLdsLayout<NP, MERGED>(T, m0).SIZE;
     const bool row = valid && i < n;
     const long bn = valid ? b * n : 0;
     const int ic = i < n ? i : n - 1; // clamped column for unconditional loads
@@ -1147,6 +1190,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         pv[it] = (c < 12) ? a.pose[base + t * 12 + c] : a.pose_ref[base + t * 12 + c - 12];
     }
     const double h_i = row ? h_i0 : 0.0;
+    const bool hint = valid && a.ws_hint[b] != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
 #pragma unroll
     for (int rr = 0; rr < kTMax * 6; ++rr)
@@ -1327,6 +1371,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         }
     }
 
+    // level-0 infeasible, or (warm start) it was last time: straight to the repair kernel
+    const bool to_rep = l0bad || hint;
     if (!active) {
         double tau_i = x_i + h_i;
         if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
@@ -1334,6 +1380,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         if (valid && i == 0) {
             a.status[b] = status;
             a.iters[b] = 0;
+            if (hint) a.ws_hint[b] = 0; // level 0 met at b0 inside the bounds
         }
     }
     if (__any(active)) {
@@ -1347,7 +1394,33 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             q1[c] = v * il[c];
         }
         if (active) a.ui_scr[b * NP + i] = u_imp; // for the level-0 repair
-        if (active) { // park (u, Q1) for the active-set kernel
+        if constexpr (MERGED) {
+            __syncthreads(); // the fast layout is dead: this LDS becomes the active-set layout
+            const ActiveLayout<NP> LA(T, m0);
+            const bool ga = active && !to_rep;
+#pragma unroll
+            for (int c = 0; c < NP; ++c) S[LA.QA + c * (NP + 1) + i] = (ga && c < M0 && c < m0) ? q1[c < M0 ? c : 0] : 0.0;
+            int st2 = 0, it2 = 0;
+            bool inf = false;
+            const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf);
+            if (active) {
+                if (inf || to_rep) {
+                    if (i == 0) {
+                        a.status[b] = -2;
+                        a.work[a.epoch * 2 + 1] = 1;
+                    }
+                } else {
+                    double tau2 = x2 + h_i;
+                    if (!isfinite(tau2) && st2 == 0) st2 = 3;
+                    if (st2 != 0) tau2 = h_i;
+                    if (row) a.tau[bn + i] = tau2;
+                    if (i == 0) {
+                        a.status[b] = st2;
+                        a.iters[b] = it2;
+                    }
+                }
+            }
+        } else if (active) { // park (u, Q1) for the active-set kernel
             double *us = a.u_scr + b * NP;
             double *qs = a.q1_scr + b * kM0Max * NP;
             us[i] = u_i;
@@ -1355,8 +1428,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             for (int c = 0; c < M0; ++c)
                 if (c < m0) qs[c * NP + i] = q1[c];
             if (i == 0) {
-                a.status[b] = l0bad ? -2 : -1; // picked up by the active-set / repair kernel
-                a.work[a.epoch * 2 + (l0bad ? 1 : 0)] = 1;
+                a.status[b] = to_rep ? -2 : -1; // picked up by the active-set / repair kernel
+                a.work[a.epoch * 2 + (to_rep ? 1 : 0)] = 1;
             }
         }
     }
@@ -1384,9 +1457,11 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
     static size_t attr_fast = 0, attr_active = 0, attr_repair = 0;
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
-    hipError_t e = launch_one<NP, FastLayout<NP>>(qppvm_fast_kernel<NP, M0>, a, grid, stream, attr_fast);
+    constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
+    hipError_t e = launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED>, a, grid, stream,
+                                                             attr_fast);
     if (e != hipSuccess) return e;
-    e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
+    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
     if (e != hipSuccess) return e;
     return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, grid, stream, attr_repair);
 }

@@ -52,6 +52,9 @@ struct wbq_ctx {
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
     double *ui_scr = nullptr, *b0_scr = nullptr; // u_imp and b0 for the level-0 repair
     int *work = nullptr; // [2][2] per-solve work flags (see wbq_kernels.h)
+    unsigned char *ws_hint = nullptr; // [B] warm start (see wbq_kernels.h)
+    signed char *ws_state = nullptr;  // [B][NP]
+    size_t np = 0;
     int epoch = 0;
 };
 
@@ -160,7 +163,10 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess &&
-             hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess;
+             hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
+             hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
+             hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
+        c->np = np;
         if (!ok) return cleanup(WBQ_E_DEVICE);
     }
 #ifdef WBQ_STAMPS
@@ -254,6 +260,8 @@ int wbq_solve(wbq_ctx *c)
     a.b0_scr = c->b0_scr;
     a.work = c->work;
     a.epoch = c->epoch;
+    a.ws_hint = c->ws_hint;
+    a.ws_state = c->ws_state;
 
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
@@ -317,10 +325,24 @@ int wbq_get_device_outputs(wbq_ctx *c, const double **tau, const int32_t **statu
 
 int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
 {
-    (void)mask;
-    // The dual active set starts cold from the unconstrained optimum every call; there is
-    // no carried working set to drop yet (the solution is unique either way).
-    return c ? WBQ_SUCCESS : WBQ_E_INVALID;
+    // Drops the per-instance warm start (repair hint + BVLS bound state), stream-ordered
+    // with the solves; a cold instance takes the default path next time.
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipSetDevice(c->device));
+    const int B = c->d.max_batch;
+    int b = 0;
+    while (b < B) {
+        if (mask && !mask[b]) {
+            ++b;
+            continue;
+        }
+        int e = b + 1;
+        while (e < B && (!mask || mask[e])) ++e;
+        WBQ_HIP(hipMemsetAsync(c->ws_hint + b, 0, (size_t)(e - b), c->stream));
+        WBQ_HIP(hipMemsetAsync(c->ws_state + (size_t)b * c->np, 0, (size_t)(e - b) * c->np, c->stream));
+        b = e;
+    }
+    return WBQ_SUCCESS;
 }
 
 int wbq_set_timing(wbq_ctx *c, int enable)
@@ -388,6 +410,8 @@ void wbq_destroy(wbq_ctx *c)
     if (c->ui_scr) (void)hipFree(c->ui_scr);
     if (c->b0_scr) (void)hipFree(c->b0_scr);
     if (c->work) (void)hipFree(c->work);
+    if (c->ws_hint) (void)hipFree(c->ws_hint);
+    if (c->ws_state) (void)hipFree(c->ws_state);
 
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;

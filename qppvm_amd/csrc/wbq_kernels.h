@@ -40,6 +40,11 @@ struct QppvmArgs {
     // clears the other parity's flags for the next solve.
     int *work;       // [2][2]
     int epoch;       // 0 / 1
+    // per-instance warm start across solves (the qpOASES hot-start analogue; it changes the
+    // path, never the solution): hint = the last solve needed the level-0 repair, so go there
+    // directly; state = BVLS bound state (-1/0/+1 per joint) of that repair
+    unsigned char *ws_hint; // [B]
+    signed char *ws_state;  // [B][NP]
 };
 
 constexpr int kStamps = 8;

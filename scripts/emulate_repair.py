@@ -112,10 +112,11 @@ def bvls(A, b, lo, hi):  # A: m x n (columns a_i)
                 if not al[i] < 1: al[i] = np.inf
             jb = int(np.argmin(al))
             if al[jb] == np.inf:
-                x[fr] = z[fr]; freed = -1; break
+                x[fr] = z[fr]; freed = -1; ex[:] = False; break
             alpha = max(al[jb], 0)
             if jb == freed and alpha == 0:
                 ex[jb] = True; st[jb] = -1 if z[jb] < lo[jb] else 1; x[jb] = lo[jb] if st[jb] < 0 else hi[jb]; break
+            ex[:] = False
             for i in np.where(fr)[0]:
                 x[i] += alpha * (z[i] - x[i])
                 if i == jb: st[i] = -1 if z[i] < lo[i] else 1
@@ -124,12 +125,14 @@ def bvls(A, b, lo, hi):  # A: m x n (columns a_i)
                 if st[i] == -1: x[i] = lo[i]
                 if st[i] == 1: x[i] = hi[i]
             freed = -1
-        w = A.T @ (b - A @ x)
+        Ax = A @ x
+        w = A.T @ (b - Ax)
+        wt = 1e-11 * max(1, np.abs(A.T @ b).max(), np.abs(A.T @ Ax).max())
         v = np.where((st != 0) & ~ex & (lo != hi), np.where(st < 0, w, -w), -np.inf)
         best = int(np.argmax(v))
         if not v[best] > wt:
             return x, it
-        st[best] = 0; freed = best; ex[:] = False
+        st[best] = 0; freed = best
 
 
 def main(n, mask, tau_max, seed, B, idx):

@@ -175,3 +175,43 @@ def test_full_size_properties(wbq_mod, oracle_lib):
     sample = {k: v[idx] for k, v in inp.items()}
     tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, sample)
     assert rel_err(tau[idx], tau_r) <= TOL
+
+
+@pytest.mark.parametrize("n", [30, 39])
+def test_warm_start_changes_path_not_result(wbq_mod, oracle_lib, n):
+    """Per-instance warm start (repair hint + BVLS state) carried across solves of one
+    context, including stale hints from a different batch, gives the cold results."""
+    prob = QPPVMProblem(n=n, tau_max=30.0)
+    x = qppvm_instances(prob, 24, seed=400 + n)
+    y = qppvm_instances(prob, 24, seed=500 + n)
+    tau_c, st_c, _ = gpu_solve(wbq_mod, prob, y)
+    s = wbq_mod.QPPVMSolver(prob, max_batch=24)
+    try:
+        s.solve_batch(x)                 # hints from x
+        tau_w, st_w, _ = s.solve_batch(y)  # stale hints on y
+        tau_w2, st_w2, _ = s.solve_batch(y)  # own hints
+        s.reset_warmstart()
+        tau_r, st_r, _ = s.solve_batch(y)
+    finally:
+        s.close()
+    for t, st in ((tau_w, st_w), (tau_w2, st_w2), (tau_r, st_r)):
+        np.testing.assert_array_equal(st, st_c)
+        assert rel_err(t, tau_c) <= 1e-9
+    tau_o, st_o, _ = oracle_lib.qppvm_batch(prob, y)
+    np.testing.assert_array_equal(st_c, st_o)
+    assert rel_err(tau_c[st_o == 0], tau_o[st_o == 0]) <= TOL
+    # stale "repair" hints on instances whose level 0 is feasible: zero task error and
+    # velocity give b0 = 0, attainable at x = 0 when |h| <= tau_max
+    z = {k: v.copy() for k, v in x.items()}
+    z["pose_ref"] = z["pose"].copy()
+    z["qd"][:] = 0.0
+    z["h"] = np.clip(z["h"], -20.0, 20.0)
+    s = wbq_mod.QPPVMSolver(prob, max_batch=24)
+    try:
+        s.solve_batch(x)
+        tau_z, st_z, _ = s.solve_batch(z)
+    finally:
+        s.close()
+    tau_zo, st_zo, _ = oracle_lib.qppvm_batch(prob, z)
+    np.testing.assert_array_equal(st_z, st_zo)
+    assert rel_err(tau_z, tau_zo) <= TOL
