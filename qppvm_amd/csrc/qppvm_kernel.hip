@@ -685,6 +685,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         __syncthreads();
         (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 8 * NP);
     }
+    WBQ_STAMP(9);
     // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)
     double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
     int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
@@ -809,6 +810,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
             }
         }
     }
+    WBQ_STAMP(10);
     // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
     if (row) a.ws_state[b * NP + i] = (signed char)(st == 2 ? 0 : st);
     double ys[M0];
@@ -1116,13 +1118,16 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
     const int n = a.n;
     const bool row = valid && i < n;
     const double h_i = row ? a.h[b * n + i] : 0.0;
+    WBQ_STAMP(8);
     const bool warm = valid && a.ws_hint[b] != 0;
     const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid, row ? a.tau_min[i] - h_i : -kInf,
                                                row ? a.tau_max[i] - h_i : kInf, warm);
+    WBQ_STAMP(11);
     int status = ro.status, iters = 0;
     bool infeasible = false;
     const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status, iters,
                                         infeasible);
+    WBQ_STAMP(12);
     if (infeasible && status == 0) status = 2;
     double tau_i = x_i + h_i;
     if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;

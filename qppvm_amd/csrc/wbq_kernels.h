@@ -47,7 +47,7 @@ struct QppvmArgs {
     signed char *ws_state;  // [B][NP]
 };
 
-constexpr int kStamps = 8;
+constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
 
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream);

@@ -30,14 +30,15 @@ def run(libpath, prob, inp, reps=20, stamps=False):
     if stamps:
         B = inp["h"].shape[0]
         nb = (B + 1) // 2 if prob.n <= 32 else B
-        buf = (ctypes.c_ulonglong * (8 * nb))()
+        K = 16
+        buf = (ctypes.c_ulonglong * (K * nb))()
         s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         assert s.lib.wbq_diag_stamps(s.ctx, buf, nb) == 0
-        st = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8)[:, [0, 1, 2, 3, 5]].astype(np.int64)
+        full = np.frombuffer(buf, dtype=np.uint64).reshape(nb, K).astype(np.int64)
+        st = full[:, [0, 1, 2, 3, 5]]
         d = np.diff(st, axis=1)
         out["fast_kernel_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in enumerate(PHASES)}
         out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
-        full = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
         _, status, iters = s.outputs()
         it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if prob.n <= 32 else iters[:nb]
         act = it_blk > 0
@@ -50,6 +51,14 @@ def run(libpath, prob, inp, reps=20, stamps=False):
             out["active_cycles_per_step_mean"] = float((loop / it_blk[act]).mean())
             out["active_block_max_steps_p50_p90_max"] = [float(np.percentile(it_blk[act], q)) for q in (50, 90, 100)]
             out["iters_hist"] = np.bincount(iters).tolist()
+        rep = full[:, 12] > full[:, 8]
+        if rep.any():
+            r = full[rep][:, 8:13]
+            d = np.diff(r, axis=1)
+            out["repair_blocks"] = int(rep.sum())
+            out["repair_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in
+                                               enumerate(["gauss-jordan A0", "bvls", "pins+equality", "dual active set"])}
+            out["repair_iters_mean"] = float(iters[: len(iters)].mean())
     s.close()
     return out
 
@@ -72,6 +81,10 @@ def main():
     free.close()
     p2 = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
     res["cfg2_B4096_stamps"] = run(diag, p2, sub, stamps=True)
+    # level-0 repair path (tight limits), warm after the first solve
+    for nn, B in ((39, 1), (39, 64), (30, 64)):
+        pr = QPPVMProblem(n=nn, tau_max=30.0)
+        res[f"repair_n{nn}_B{B}"] = run(diag, pr, qppvm_instances(pr, B, seed=7), stamps=True)
     print(json.dumps(res, indent=1))
 
 
