@@ -15,15 +15,16 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
-SRC = os.path.join(HERE, "wbq_oracle.c")
+SRCS = [os.path.join(HERE, f) for f in ("wbq_oracle.c", "wbq_oracle_contact.c")]
 
 
 def build(force: bool = False) -> str:
     """Compile the C restatement with gcc (host only)."""
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(
-            os.path.getmtime(SRC), os.path.getmtime(os.path.join(HERE, "wbq_oracle.h"))):
+    deps = SRCS + [os.path.join(HERE, "wbq_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, deps)):
         subprocess.check_call(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-Wall", "-Wextra",
-                               "-Wno-unused-parameter", SRC, "-o", LIB_PATH, "-lm"])
+                               "-Wno-unused-parameter", *SRCS, "-o", LIB_PATH + ".tmp", "-lm"])
+        os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 
 
@@ -56,6 +57,14 @@ def lib():
         _lib.wbq_ref_qppvm_one.argtypes = [P, P, P, P, P]
         _lib.wbq_ref_qppvm_one.restype = ctypes.c_int
         _lib.wbq_ref_qppvm_batch.argtypes = [P, ctypes.c_int] + [P] * 8 + [P, P, P]
+        I = ctypes.c_int
+        _lib.wbq_ref_dual_qp.argtypes = [I, P, P, I, P, P, I, P, P, P, P, P]
+        _lib.wbq_ref_dual_qp.restype = I
+        _lib.wbq_ref_contact_assemble.argtypes = [P, P] + [P] * 8
+        _lib.wbq_ref_contact_assemble.restype = I
+        _lib.wbq_ref_contact_one.argtypes = [P, P, P, P, P, P]
+        _lib.wbq_ref_contact_one.restype = I
+        _lib.wbq_ref_contact_batch.argtypes = [P, I] + [P] * 14 + [P, P, P, P, P]
     return _lib
 
 
@@ -148,3 +157,91 @@ def qppvm_batch(prob, inputs):
     lib().wbq_ref_qppvm_batch(ctypes.byref(d), B, *[_p(a) for a in arrs], _p(tau), _p(status),
                               _p(iters))
     return tau, status, iters
+
+
+# ------------------------------------------------------------------ contact form (ForceAcc)
+class _CDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("n_fb", ctypes.c_int), ("nc", ctypes.c_int),
+                ("Kp_w", ctypes.c_double), ("Kd_w", ctypes.c_double), ("Kp_f", ctypes.c_double),
+                ("Kd_f", ctypes.c_double), ("Kp_p", ctypes.c_double), ("Kd_p", ctypes.c_double),
+                ("f_lb", ctypes.c_double * 3), ("f_ub", ctypes.c_double * 3), ("eps_f", ctypes.c_double),
+                ("torque_rows", ctypes.c_int), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+
+
+class _CInst(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w",
+                                               "pose_w_ref", "Jc", "jdqd_c", "pose_c", "pose_c_ref")] + \
+               [("contact_mask", ctypes.c_int)]
+
+
+CONTACT_ARRAYS = ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref", "Jc", "jdqd_c",
+                  "pose_c", "pose_c_ref")
+
+
+def _cdesc(prob):
+    d = _CDesc()
+    d.n, d.n_fb, d.nc = prob.n, prob.n_fb, prob.nc
+    for k in ("Kp_w", "Kd_w", "Kp_f", "Kd_f", "Kp_p", "Kd_p", "eps_f"):
+        setattr(d, k, float(getattr(prob, k)))
+    for k in range(3):
+        d.f_lb[k], d.f_ub[k] = prob.f_lb[k], prob.f_ub[k]
+    d.torque_rows = int(bool(prob.torque_rows))
+    keep = [np.ascontiguousarray(prob.tau_max, dtype=np.float64), np.ascontiguousarray(prob.tau_min, dtype=np.float64)]
+    d.tau_max, d.tau_min = keep[0].ctypes.data, keep[1].ctypes.data
+    return d, keep
+
+
+def _cinst(inputs, b):
+    s = _CInst()
+    arrs = [np.ascontiguousarray(inputs[k][b], dtype=np.float64) for k in CONTACT_ARRAYS]
+    for k, a in zip(CONTACT_ARRAYS, arrs):
+        setattr(s, k, a.ctypes.data)
+    s.contact_mask = int(inputs["cmask"][b])
+    return s, arrs
+
+
+def dual_qp(H, g, E, e, C, clo, chi):
+    """Dense dual active-set QP (oracle): min 0.5 x'Hx + g'x, E x = e, clo <= C x <= chi."""
+    n = H.shape[0]
+    H, g, E, e = _c(H), _c(g), _c(E).reshape(-1, n), _c(e)
+    C, clo, chi = _c(C).reshape(-1, n), _c(clo), _c(chi)
+    x = np.zeros(n)
+    it = ctypes.c_int(0)
+    st = lib().wbq_ref_dual_qp(n, _p(H), _p(g), E.shape[0], _p(E), _p(e), C.shape[0], _p(C), _p(clo), _p(chi),
+                               _p(x), ctypes.byref(it))
+    return x, st, it.value
+
+
+def contact_assemble(prob, inputs, b=0):
+    d, keep = _cdesc(prob)
+    s, arrs = _cinst(inputs, b)
+    nx = prob.nx
+    mi = 3 * prob.nc + (prob.n - prob.n_fb if prob.torque_rows else 0)
+    H, g, E, e = np.zeros((nx, nx)), np.zeros(nx), np.zeros((12, nx)), np.zeros(12)
+    C, clo, chi, bw = np.zeros((max(mi, 1), nx)), np.zeros(max(mi, 1)), np.zeros(max(mi, 1)), np.zeros(6)
+    lib().wbq_ref_contact_assemble(ctypes.byref(d), ctypes.byref(s), _p(H), _p(g), _p(E), _p(e), _p(C),
+                                   _p(clo), _p(chi), _p(bw))
+    return dict(H=H, g=g, E=E, e=e, C=C[:mi], clo=clo[:mi], chi=chi[:mi], bw=bw)
+
+
+def contact_one(prob, inputs, b=0):
+    d, keep = _cdesc(prob)
+    s, arrs = _cinst(inputs, b)
+    tau, x = np.zeros(prob.n), np.zeros(prob.nx)
+    it, rep = ctypes.c_int(0), ctypes.c_int(0)
+    st = lib().wbq_ref_contact_one(ctypes.byref(d), ctypes.byref(s), _p(tau), _p(x), ctypes.byref(it),
+                                   ctypes.byref(rep))
+    return dict(tau=tau, x=x, status=st, iters=it.value, l0_repaired=rep.value)
+
+
+def contact_batch(prob, inputs):
+    """tau[B, n], x[B, nx], status[B], iters[B], l0_repaired[B] (single thread)."""
+    d, keep = _cdesc(prob)
+    arrs = [_c(inputs[k]) for k in CONTACT_ARRAYS]
+    cm = np.ascontiguousarray(inputs["cmask"], dtype=np.int32)
+    B = arrs[1].shape[0]
+    tau, x = np.zeros((B, prob.n)), np.zeros((B, prob.nx))
+    st, it, rep = (np.zeros(B, dtype=np.int32) for _ in range(3))
+    lib().wbq_ref_contact_batch(ctypes.byref(d), B, *[_p(a) for a in arrs], _p(cm), _p(tau), _p(x), _p(st),
+                                _p(it), _p(rep))
+    return tau, x, st, it, rep

@@ -113,6 +113,54 @@ void wbq_ref_qppvm_batch(const wbq_ref_desc *d, int B, const double *M, const do
                          const double *qd, const double *qref, const double *h, double *tau,
                          int32_t *status, int32_t *iters);
 
+/* ---------------------------------------------------------------- contact form (ForceAcc)
+ * SURVEY.md 8a rows a10-a12; spec in wbq_oracle_contact.c. x = [qdd (n); f (3 per contact)]. */
+#define WBQ_REF_MAX_CONTACTS 4
+typedef struct {
+    int n;              /* DoF including the n_fb floating-base coordinates (first) */
+    int n_fb;           /* 6 */
+    int nc;             /* contacts, <= WBQ_REF_MAX_CONTACTS */
+    double Kp_w, Kd_w;  /* waist acceleration task gains */
+    double Kp_f, Kd_f;  /* feet acceleration task gains */
+    double Kp_p, Kd_p;  /* postural task gains */
+    double f_lb[3], f_ub[3]; /* force box of an active contact (ForceAcc.cpp:74-76) */
+    double eps_f;       /* min-norm tie-break weight on the forces */
+    int torque_rows;    /* a12 extension: actuated torque-limit rows */
+    const double *tau_max, *tau_min; /* [n] (rows n_fb.. used when torque_rows) */
+} wbq_ref_contact_desc;
+
+/* One instance: M [n][n], h, q, qd, qref [n]; waist Jw [6][n], jdqd_w [6] (Jdot qd),
+ * pose_w / pose_w_ref [12]; contacts Jc [nc][6][n], jdqd_c [nc][6], pose_c / pose_c_ref
+ * [nc][12]; contact_mask bit c = contact c active (inactive: f_c = 0). */
+typedef struct {
+    const double *M, *h, *q, *qd, *qref;
+    const double *Jw, *jdqd_w, *pose_w, *pose_w_ref;
+    const double *Jc, *jdqd_c, *pose_c, *pose_c_ref;
+    int contact_mask;
+} wbq_ref_contact_instance;
+
+/* Dense Goldfarb-Idnani dual active set, KKT re-solved by LU each step:
+ *   min 0.5 x^T H x + g^T x  s.t.  E x = e (me rows),  clo <= C x <= chi (mi rows),  H SPD. */
+int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const double *E, const double *e,
+                    int mi, const double *C, const double *clo, const double *chi, double *x, int *iters);
+
+/* Level-1 data of the contact form (nx = n + 3 nc): H1, g1, E [12][nx] (waist rows with
+ * rhs b_w, then dynamic feasibility), C [mi][nx] with clo/chi; bw [6] the waist target.
+ * Returns mi. */
+int wbq_ref_contact_assemble(const wbq_ref_contact_desc *d, const wbq_ref_contact_instance *in, double *H1,
+                             double *g1, double *E, double *e, double *C, double *clo, double *chi, double *bw);
+
+/* Whole chain for one instance: tau = M qdd + h - sum_c J_c^T [f_c; 0] (tau = h on failure),
+ * x = [qdd; f]. l0_repaired = 1 when level 0 is not attainable at b_w (y0* != b_w). */
+int wbq_ref_contact_one(const wbq_ref_contact_desc *d, const wbq_ref_contact_instance *in, double *tau,
+                        double *x, int *iters, int *l0_repaired);
+
+void wbq_ref_contact_batch(const wbq_ref_contact_desc *d, int B, const double *M, const double *h, const double *q,
+                           const double *qd, const double *qref, const double *Jw, const double *jdqd_w,
+                           const double *pose_w, const double *pose_w_ref, const double *Jc, const double *jdqd_c,
+                           const double *pose_c, const double *pose_c_ref, const int32_t *cmask, double *tau,
+                           double *x, int32_t *status, int32_t *iters, int32_t *l0_repaired);
+
 #ifdef __cplusplus
 }
 #endif

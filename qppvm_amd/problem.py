@@ -127,3 +127,84 @@ def check_inputs(prob: QPPVMProblem, inputs: dict) -> int:
         if a.dtype != np.float64:
             raise ValueError(f"input {k}: expected float64, got {a.dtype}")
     return B
+
+
+# ------------------------------------------------------------------ contact form (ForceAcc)
+@dataclass
+class ContactProblem:
+    """Batch-shared structure of the ForceAcc contact-form stack (reference
+    ``src/ForceAcc.cpp``):
+
+    * variables ``x = [qdd (n); f_c (3) per contact]`` (``:58-72``), wrench ``[f; 0_3]`` (``:81``);
+    * level 0 = waist (pelvis) acceleration task (``:118-122``);
+    * level 1 = postural + feet acceleration tasks (``:83-89``, ``:105-107``, ``:131``)
+      + ``eps_f ||f||^2``, the explicit minimum-norm tie-break on the contact forces;
+    * both levels: DynamicFeasibility on the ``n_fb`` floating-base rows (``:109-114``),
+      force box ``f_lb <= f <= f_ub`` (``:74-76``), zero force for inactive contacts,
+      and (``torque_rows``, row a12, an extension) actuated torque limits;
+    * ``tau = M qdd + h - sum_c J_c^T [f_c; 0]`` (``:206-218``).
+
+    The acceleration-task gains are OpenSoT defaults upstream (not in the reference); here
+    they are named options (critically damped unit stiffness by default).
+    """
+
+    n: int
+    nc: int = 2
+    n_fb: int = 6
+    Kp_w: float = 1.0
+    Kd_w: float = 2.0
+    Kp_f: float = 1.0
+    Kd_f: float = 2.0
+    Kp_p: float = 1.0
+    Kd_p: float = 2.0
+    f_lb: tuple = (-1000.0, -1000.0, 10.0)
+    f_ub: tuple = (1000.0, 1000.0, 1000.0)
+    eps_f: float = 1e-8
+    torque_rows: bool = False
+    tau_max: np.ndarray | float = 150.0
+    tau_min: np.ndarray | float | None = None
+    max_iter: int = 0  # 0 = default cap
+
+    def __post_init__(self):
+        n, nc = int(self.n), int(self.nc)
+        if not (1 <= nc <= 4):
+            raise ValueError("nc must be in [1, 4]")
+        if self.n_fb != 6 or n <= self.n_fb:
+            raise ValueError("the contact form needs a 6-DoF floating base and n > 6")
+        if n + 3 * nc > 64:
+            raise ValueError("n + 3 nc must be <= 64 (one instance per wavefront)")
+        if not self.eps_f > 0:
+            raise ValueError("eps_f must be > 0")
+        self.n, self.nc = n, nc
+        self.f_lb = tuple(float(v) for v in self.f_lb)
+        self.f_ub = tuple(float(v) for v in self.f_ub)
+        self.tau_max = _vec(self.tau_max, n, "tau_max")
+        self.tau_min = -self.tau_max if self.tau_min is None else _vec(self.tau_min, n, "tau_min")
+
+    @property
+    def nx(self) -> int:
+        return self.n + 3 * self.nc
+
+
+CONTACT_INPUT_FIELDS = ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref",
+                        "Jc", "jdqd_c", "pose_c", "pose_c_ref", "cmask")
+
+
+def contact_input_shapes(prob: ContactProblem, B: int) -> dict:
+    n, nc = prob.n, prob.nc
+    return {"M": (B, n, n), "h": (B, n), "q": (B, n), "qd": (B, n), "qref": (B, n),
+            "Jw": (B, 6, n), "jdqd_w": (B, 6), "pose_w": (B, 12), "pose_w_ref": (B, 12),
+            "Jc": (B, nc, 6, n), "jdqd_c": (B, nc, 6), "pose_c": (B, nc, 12), "pose_c_ref": (B, nc, 12),
+            "cmask": (B,)}
+
+
+def check_contact_inputs(prob: ContactProblem, inputs: dict) -> int:
+    B = int(np.asarray(inputs["h"]).shape[0])
+    for k, shp in contact_input_shapes(prob, B).items():
+        a = inputs[k]
+        if tuple(a.shape) != shp:
+            raise ValueError(f"input {k}: expected shape {shp}, got {tuple(a.shape)}")
+        want = np.int32 if k == "cmask" else np.float64
+        if a.dtype != want:
+            raise ValueError(f"input {k}: expected {np.dtype(want).name}, got {a.dtype}")
+    return B

@@ -83,3 +83,53 @@ def qppvm_instances(prob: QPPVMProblem, B: int, seed: int = 0, offset: int = 0,
 def replicate(inputs: dict, B: int) -> dict:
     """Config 1: B identical copies of instance 0."""
     return {k: np.ascontiguousarray(np.broadcast_to(v[:1], (B,) + v.shape[1:])) for k, v in inputs.items()}
+
+
+def contact_instances(prob, B: int, seed: int = 0, offset: int = 0, masks=None, cond_max: float = 1e3) -> dict:
+    """Synthetic floating-base states for the contact form. Per instance:
+    M as in qppvm_instances; h ~ N(0, 10^2) with the floating-base rows carrying a
+    weight-like +z component; waist Jacobian = [R_w-blocks | 0] (the base link moves with
+    the floating base only); feet Jacobians ~ N(0, 0.5^2); Jdot qd ~ N(0, 1); poses Haar,
+    references perturbed; ``masks``: None = all contacts active, else a list of allowed
+    contact masks drawn uniformly per instance (config 2: 2, 3 or 4 feet)."""
+    n, nc = prob.n, prob.nc
+    out = {k: [] for k in ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref",
+                           "Jc", "jdqd_c", "pose_c", "pose_c_ref", "cmask")}
+    CH = 256
+    first, last = offset // CH, (offset + B - 1) // CH if B > 0 else -1
+    for c in range(first, last + 1):
+        rng = _rng(seed, (1 << 20) + c)
+        Q = _haar(rng, CH, n)
+        lam = np.exp(rng.uniform(np.log(1e-2), np.log(1e-2 * cond_max), (CH, n)))
+        M = (Q * lam[:, None, :]) @ Q.transpose(0, 2, 1)
+        M = 0.5 * (M + M.transpose(0, 2, 1))
+        h = rng.normal(0.0, 10.0, (CH, n))
+        h[:, 2] += 50.0  # gravity on the base z row: the feet push up (f_z >= 10)
+        R = _haar(rng, CH * (1 + nc), 3).reshape(CH, 1 + nc, 3, 3)
+        det = np.linalg.det(R)
+        R[det < 0, :, 0] *= -1.0
+        Jw = np.zeros((CH, 6, n))
+        Jw[:, :3, :3] = R[:, 0]
+        Jw[:, 3:, 3:6] = R[:, 0]
+        Jw[:, :3, 3:6] = rng.normal(0.0, 0.2, (CH, 3, 3))
+        Jc = rng.normal(0.0, 0.5, (CH, nc, 6, n))
+        p = rng.uniform(-1.0, 1.0, (CH, 1 + nc, 3))
+        Rref = _rotvec_to_R(rng.normal(0.0, 0.05, (CH, 1 + nc, 3))) @ R
+        pref = p + rng.normal(0.0, 0.05, (CH, 1 + nc, 3))
+        poses, poses_ref = _pose(R, p), _pose(Rref, pref)
+        q = rng.uniform(-np.pi, np.pi, (CH, n))
+        qref = q + rng.normal(0.0, 0.1, (CH, n))
+        qd = rng.normal(0.0, 1.0, (CH, n))
+        jw = rng.normal(0.0, 1.0, (CH, 6))
+        jc = rng.normal(0.0, 1.0, (CH, nc, 6))
+        if masks is None:
+            cm = np.full(CH, (1 << nc) - 1, dtype=np.int32)
+        else:
+            cm = np.asarray(masks, dtype=np.int32)[rng.integers(0, len(masks), CH)]
+        lo = max(offset, c * CH) - c * CH
+        hi = min(offset + B, (c + 1) * CH) - c * CH
+        for k, v in (("M", M), ("h", h), ("q", q), ("qd", qd), ("qref", qref), ("Jw", Jw), ("jdqd_w", jw),
+                     ("pose_w", poses[:, 0]), ("pose_w_ref", poses_ref[:, 0]), ("Jc", Jc), ("jdqd_c", jc),
+                     ("pose_c", poses[:, 1:]), ("pose_c_ref", poses_ref[:, 1:]), ("cmask", cm)):
+            out[k].append(v[lo:hi])
+    return {k: np.ascontiguousarray(np.concatenate(v, axis=0)) for k, v in out.items()}

@@ -44,3 +44,16 @@ def oracle_lib():
     import oracle
     oracle.build()
     return oracle
+
+
+def load_golden_contact(n):
+    """Yield (group, ContactProblem, inputs, expected) from tests/golden/contact_n{n}.npz."""
+    from qppvm_amd.problem import ContactProblem, CONTACT_INPUT_FIELDS
+    z = np.load(os.path.join(GOLDEN, f"contact_n{n}.npz"))
+    for g in z["groups"]:
+        g = str(g)
+        pre = g + "__"
+        prob = ContactProblem(n=n, nc=int(z[pre + "nc"]), torque_rows=bool(z[pre + "torque_rows"]),
+                              tau_max=z[pre + "tau_max"])
+        inp = {k: np.ascontiguousarray(z[pre + k]) for k in CONTACT_INPUT_FIELDS}
+        yield g, prob, inp, {"tau": z[pre + "tau"], "x": z[pre + "x"]}
