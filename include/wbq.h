@@ -23,6 +23,18 @@
  *   wbq_reset_warmstart <- qpOASES hot-start state reset (QPOases_sot re-init) [upstream].
  *   wbq_destroy       <- plugin close()/destructor (:339-342).
  *
+ * Contact form (ForceAcc plugin, src/ForceAcc.cpp):
+ *   wbq_create_contact      <- ForceAccExample::init_control_plugin's wiring (:31-141: OptvarHelper
+ *                              x = [qddot; f_c] :58-72, wrench bounds :74-95, feet tasks :83-89,
+ *                              postural :105-107, DynamicFeasibility :109-114, waist :118-122,
+ *                              AutoStack :131-133, QPOases_sot(.., 1e4) :135-137).
+ *   wbq_set_contact_inputs  <- sync_model + autostack->update (:172-184; M, h, Jacobians, poses).
+ *   wbq_solve               <- solver->solve(x) (:188-189) + the ID post-step
+ *                              tau = M qdd + h - sum_c J_c^T [f_c; 0] (:196-219).
+ *   wbq_get_contact_outputs <- the unpacked x = [qdd; f_c] (:196-201).
+ *   wbq_get_outputs         <- tau handed to setJointEffort (:219) + per-instance status; on
+ *                              status != 0 the reference skips the send (:189-193), here tau = h.
+ *
  * Conventions: fp64, row-major, instance-major contiguous arrays:
  *   M [B][n][n] SPD joint-space inertia        J [B][ntasks][6][n] (rows 0-2 linear, 3-5 angular)
  *   pose, pose_ref [B][ntasks][12] = [R | p] 3x4 row-major (Eigen::Affine3d::matrix() top rows)
@@ -54,7 +66,8 @@ extern "C" {
 #define WBQ_STATUS_NUMERICAL 3
 
 /* problem forms */
-#define WBQ_FORM_QPPVM 0 /* QPPVMPlugin: 2-level torque-space impedance QP */
+#define WBQ_FORM_QPPVM 0   /* QPPVMPlugin: 2-level torque-space impedance QP */
+#define WBQ_FORM_CONTACT 1 /* ForceAccExample: 2-level acceleration + contact-force QP */
 
 /* Cartesian row selection semantics of OpenSoT::Indices::range(0,2) (QPPVMPlugin.cpp:134) */
 #define WBQ_SELECT_SUBTASK 0 /* full 6-D task built, rows selected afterwards */
@@ -93,14 +106,47 @@ typedef struct {
     const double *M, *J, *pose, *pose_ref, *q, *qd, *qref, *h;
 } wbq_inputs;
 
+/* Contact form: x = [qdd (n); f_c (3 per contact)] (ForceAcc.cpp:58-72); level 0 = waist
+ * acceleration task, level 1 = postural + feet acceleration tasks + eps_f ||f||^2 (the explicit
+ * minimum-norm tie-break of the internal forces); both levels: dynamic feasibility on the 6
+ * floating-base rows, force box for active contacts (f = 0 for inactive ones), optional
+ * actuated torque rows tau_min <= M_a qdd + h_a - J_c,a^T f <= tau_max. */
+typedef struct {
+    int n;            /* DoF incl. the floating base (first n_fb coordinates); n + 6 + 3 nc <= 64 */
+    int n_fb;         /* must be 6 */
+    int nc;           /* contacts, 1..4 */
+    int torque_rows;  /* 0/1 */
+    int max_batch;
+    int max_iter;     /* 0 = default 10 (nx + m) + 50 */
+    double Kp_w, Kd_w, Kp_f, Kd_f, Kp_p, Kd_p; /* waist / feet / postural task gains */
+    double f_lb[3], f_ub[3];                   /* force box (reference: -1000,-1000,10 / 1000) */
+    double eps_f;                              /* > 0 */
+    const double *tau_max, *tau_min;           /* [n] (used with torque_rows) */
+} wbq_contact_desc;
+
+/* Contact-form batch, fp64 row-major, instance-major:
+ *   M [B][n][n], h, q, qd, qref [B][n], Jw [B][6][n], jdqd_w [B][6], pose_w, pose_w_ref [B][12],
+ *   Jc [B][nc][6][n], jdqd_c [B][nc][6], pose_c, pose_c_ref [B][nc][12], cmask [B] (bit c = active). */
+typedef struct {
+    int batch;
+    int memory;
+    const double *M, *h, *q, *qd, *qref, *Jw, *jdqd_w, *pose_w, *pose_w_ref;
+    const double *Jc, *jdqd_c, *pose_c, *pose_c_ref;
+    const int32_t *cmask;
+} wbq_contact_inputs;
+
 int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out);
+int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out);
 /* Launch on a caller-provided hipStream_t (NULL = the context's own stream). */
 int wbq_set_stream(wbq_ctx *ctx, void *hip_stream);
 int wbq_set_inputs(wbq_ctx *ctx, const wbq_inputs *in);
+int wbq_set_contact_inputs(wbq_ctx *ctx, const wbq_contact_inputs *in);
 int wbq_solve(wbq_ctx *ctx);
 int wbq_sync(wbq_ctx *ctx);
 /* Synchronous copy of the last solve's outputs to host memory (any pointer may be NULL). */
 int wbq_get_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
+/* Contact form: synchronous copy of the last solve's x = [qdd; f] ([batch][n + 3 nc]). */
+int wbq_get_contact_outputs(wbq_ctx *ctx, double *x);
 /* Write outputs into caller-owned device buffers ([batch][n] / [batch]) instead of the
  * context's (any NULL pointer reverts that output to the context buffer). */
 int wbq_set_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);

@@ -1,0 +1,587 @@
+// contact_kernel.hip -- batched contact-form (ForceAcc) whole-body QP for gfx950 (MI355X), fp64.
+//
+// One instance per wave64 block. The math (reference
+// src/ForceAcc.cpp; the build's written spec is oracle/wbq_oracle_contact.c):
+//   x = [qdd (n); f_c (3) per contact]                                     (:58-72)
+//   level 0   min ||J_w qdd - b_w||^2             (waist / pelvis task)       (:118-122)
+//   level 1   min ||qdd - b_p||^2 + sum_c ||J_c qdd - b_c||^2 + eps_f ||f||^2 (:83-89, :105-107)
+//             s.t. J_w qdd = y0* = b_w (level 0 attained, the generic case)
+//   both      M_fb qdd - sum_c J_c[0:3, fb]^T f_c = -h_fb   (DynamicFeasibility, :109-114)
+//             f_lb <= f_c <= f_ub for active contacts, f_c = 0 otherwise  (:74-76, :91-95)
+//             optional actuated torque rows tau_min <= M_a qdd + h_a - J_ca^T f <= tau_max (a12)
+//   tau = M qdd + h - sum_c J_c^T [f_c; 0]                                  (:206-218)
+// with Cartesian acceleration tasks J qdd = Kp e - Kd J qd - Jdot qd and the postural task
+// qdd = Kp (q_ref - q) - Kd qd.
+//
+// Method: Goldfarb-Idnani dual active set carried entirely in constraint space. With
+// H = blockdiag(I + sum_c J_c^T J_c, eps_f I) and the m constraint rows A,
+//   Gamma = A H^-1 A^T (m x m),  s = A x (m activities),
+// one lane per constraint row runs every step: the active-set Gram is Gamma_AA = L L^T with
+// T = L^-1 kept in LDS (an add appends one row of T in closed form, a drop re-appends the
+// rows after it), and x is rebuilt once at the end from the multipliers,
+// x = H^-1 (A^T lambda - g). H^-1 A^T comes from one block Gauss-Jordan on the qdd block of
+// H (lane i <-> joint i, the right-hand sides are M's rows and J_w's columns); the force
+// block is diagonal. Gamma mixes O(1) acceleration terms with O(1/eps_f) force terms, so the
+// active-set arithmetic is only good to ~cond(Gamma) * 1e-16; two steps of iterative
+// refinement of (x, lambda) on the final active set, with the residual of the active rows
+// taken exactly in x-space, restore full fp64 accuracy (scripts/emulate_contact.py: 1e-5
+// relative without, 1e-12 with). A final re-check of every row guards the active set itself.
+//
+// Joint rows double as the torque output: tau_i = (row i of [M | -J_lin^T]) x + h_i, the
+// activity of joint row i, whether or not it is a constraint.
+//
+// Statuses: 0 ok, 1 step cap, 2 infeasible (level 0 not attainable at b_w, or no feasible
+// point), 3 numerical. On status != 0: tau = h, x = 0.
+#include "wbq_kernels.h"
+#include "wbq_device.h"
+
+namespace wbq {
+namespace {
+
+// Per-instance LDS layout in doubles. Compact constraint index ci (= GI lane):
+//   ci <  NJ             joint row a = ci (a < 6: dynamic feasibility, an equality;
+//                        a >= 6: actuated torque row, only with torque rows, NJ = n)
+//   NJ <= ci < NJ + 6    waist row r = ci - NJ (equality, target b_w)
+//   NJ + 6 <= ci < ME    force row f = ci - NJ - 6 (box; disabled for inactive contacts)
+// X = H^-1 A_q^T has one column ("slot") per q-bearing row, slot = ci, plus x0 at NJ + 6.
+struct ContactLayout {
+    int NJ, NR, ME, NX, QS, FS, GS, TS;
+    int AQJ, AQW, FFJ, XT, GM, TT, JC, PN, RH, HR, XV, X0, VV, LV, RV, AC, PS, BT, JD, QD, SIZE;
+    __host__ __device__ ContactLayout(int n, int nc, bool tr, int NQ, int NRC)
+    {
+        NJ = tr ? n : 6;
+        NR = NJ + 7;
+        ME = NJ + 6 + 3 * nc;
+        NX = n + 3 * nc;
+        QS = NQ + 1;          // row stride of NQ-wide rows (odd: lane-per-row reads conflict-free)
+        FS = 3 * nc + 1;
+        GS = ME | 1;
+        TS = NX | 1;          // the active set never exceeds NX independent rows
+        int o = 0;
+        AQJ = o; o += n * QS;     // joint rows, acceleration part: M row a
+        AQW = o; o += 6 * QS;     // waist rows: J_w row r
+        FFJ = o; o += n * FS;     // joint rows, force part: -J_c[0:3, a] (active contacts)
+        XT = o; o += NR * QS;     // X^T: slot s = column s of H^-1 A_q^T over the qdd lanes
+        GM = o; o += ME * GS;     // Gamma
+        TT = o;                   // T = L^-1 of the active-set Gram, rows of TS
+        int ov = 0;               // setup-phase overlays of the TT region
+        JC = TT + ov; ov += 6 * kCMax * NQ;   // contact Jacobian rows
+        PN = TT + ov; ov += 2 * 64 * 4;       // Gauss-Jordan pivot panel
+        RH = TT + ov; ov += 2 * 4 * NRC;      // its right-hand sides
+        HR = TT + ov; ov += (NQ == 64 && tr) ? NQ * QS : 0; // H rows for a second rhs chunk
+        const int tt = NX * TS;
+        o += tt > ov ? tt : ov;
+        XV = o; o += 64;          // x
+        X0 = o; o += 64;          // x0 = -H^-1 g
+        VV = o; o += 64;
+        LV = o; o += 64;
+        RV = o; o += 64;
+        AC = o; o += 64;          // active constraint (compact index) per slot
+        PS = o; o += 24 * (1 + kCMax);   // poses: waist, then contacts ([R|p], ref)
+        BT = o; o += 6 * (1 + kCMax);    // task targets: waist b_w, then b_c
+        JD = o; o += 6 * (1 + kCMax);    // Jdot qd
+        QD = o; o += 64;
+        SIZE = (o + 1) & ~1;
+    }
+};
+
+// acceleration part of constraint row ci (nullptr: none, i.e. a force row)
+__device__ __forceinline__ const double *row_q(const double *S, const ContactLayout &L, int ci)
+{
+    if (ci < L.NJ) return S + L.AQJ + ci * L.QS;
+    if (ci < L.NJ + 6) return S + L.AQW + (ci - L.NJ) * L.QS;
+    return nullptr;
+}
+
+// force coefficient of row ci on force variable f
+__device__ __forceinline__ double fcoef(const double *S, const ContactLayout &L, int ci, int f)
+{
+    if (ci < L.NJ) return S[L.FFJ + ci * L.FS + f];
+    if (ci < L.NJ + 6) return 0.0;
+    return (ci - L.NJ - 6 == f) ? 1.0 : 0.0;
+}
+
+// activity a_ci . x of constraint row ci at x = XV (n qdd entries, then nf forces)
+__device__ __forceinline__ double activity(const double *S, const ContactLayout &L, int ci, int n, int nf)
+{
+    const double *xv = S + L.XV;
+    double s = 0.0;
+    const double *rq = row_q(S, L, ci);
+    if (rq) {
+        for (int j = 0; j < n; ++j) s = fma(rq[j], xv[j], s);
+    }
+    if (ci < L.NJ) {
+        for (int f = 0; f < nf; ++f) s = fma(S[L.FFJ + ci * L.FS + f], xv[n + f], s);
+    } else if (ci >= L.NJ + 6) {
+        s = xv[n + ci - L.NJ - 6];
+    }
+    return s;
+}
+
+// Append slot a (compact row c, sign sg) to T = L^-1 of the active-set Gram: with
+// v_c' = sg_c' sg Gamma[act_c'][c] (c' < a), l = T v, d^2 = Gamma_cc - l.l, the new row is
+// [-(T^T l)^T / d, 1/d]. Returns d^2 (<= 0: dependent). Lane i < a owns slot i.
+__device__ __forceinline__ double t_append(double *S, const ContactLayout &L, int i, int a, int c, double sg,
+                                           int act, double sgn)
+{
+    if (i < a) S[L.VV + i] = sgn * sg * S[L.GM + act * L.GS + c];
+    __syncthreads();
+    double l = 0.0;
+    if (i < a)
+        for (int q = 0; q <= i; ++q) l = fma(S[L.TT + i * L.TS + q], S[L.VV + q], l);
+    S[L.LV + i] = l;
+    __syncthreads();
+    double r = 0.0;
+    if (i < a)
+        for (int q = i; q < a; ++q) r = fma(S[L.TT + q * L.TS + i], S[L.LV + q], r);
+    const double d2 = S[L.GM + c * L.GS + c] - isum<64>(l * l);
+    const double id = d2 > 0.0 ? frsq(d2) : 0.0;
+    if (i < a) S[L.TT + a * L.TS + i] = -r * id;
+    if (i == a) S[L.TT + a * L.TS + a] = id;
+    __syncthreads();
+    return d2;
+}
+
+// x = x0 + H^-1 A_A^T (sgn lam), then two steps of iterative refinement of (x, lambda) on the
+// active set: residual of the active rows in x-space (exact to roundoff), correction through
+// the same T. Lane i < k owns slot i; lane v < NX owns x_v. Leaves x in XV.
+__device__ __noinline__ void rebuild_refine(double *S, const ContactLayout &L, int i, int k, int n, int nf, int act,
+                                            double sgn, double &lam, double lo, double hi, double ieps)
+{
+    const int NJ = L.NJ;
+    // shuffles with every lane active (the source lane of a slot is any constraint lane)
+    const double lo_a = __shfl(lo, act), hi_a = __shfl(hi, act);
+    S[L.RV + i] = i < k ? sgn * lam : 0.0;
+    S[L.AC + i] = (double)act;
+    __syncthreads();
+    for (int pass = 0; pass < 3; ++pass) {
+        if (pass > 0) {
+            __syncthreads();
+            double res = 0.0;
+            if (i < k) res = sgn * ((sgn > 0.0 ? lo_a : hi_a) - activity(S, L, act, n, nf));
+            S[L.VV + i] = res;
+            __syncthreads();
+            double y = 0.0;
+            if (i < k)
+                for (int q = 0; q <= i; ++q) y = fma(S[L.TT + i * L.TS + q], S[L.VV + q], y);
+            S[L.LV + i] = y;
+            __syncthreads();
+            double dl = 0.0;
+            if (i < k)
+                for (int q = i; q < k; ++q) dl = fma(S[L.TT + q * L.TS + i], S[L.LV + q], dl);
+            lam += dl;
+            S[L.RV + i] = i < k ? sgn * dl : 0.0;
+            __syncthreads();
+        }
+        if (i < L.NX) {
+            double dx = 0.0;
+            if (i < n) {
+                for (int q = 0; q < k; ++q) {
+                    const int c = (int)S[L.AC + q];
+                    if (c < NJ + 6) dx = fma(S[L.RV + q], S[L.XT + c * L.QS + i], dx);
+                }
+            } else {
+                for (int q = 0; q < k; ++q) dx = fma(S[L.RV + q], fcoef(S, L, (int)S[L.AC + q], i - n), dx);
+                dx *= ieps;
+            }
+            S[L.XV + i] = (pass == 0 ? (i < n ? S[L.X0 + i] : 0.0) : S[L.XV + i]) + dx;
+        }
+    }
+    __syncthreads();
+}
+
+template <int NQ, bool TR>
+__global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const ContactArgs a)
+{
+    constexpr int NRC = TR ? 40 : 16; // Gauss-Jordan right-hand sides per pass
+    extern __shared__ __attribute__((aligned(16))) double S[];
+    const int n = a.n, nc = a.nc, nf = 3 * nc;
+    const ContactLayout L(n, nc, TR, NQ, NRC);
+    const int i = threadIdx.x;
+    const long b = blockIdx.x;
+    const int cm = a.cmask[b];
+    const bool qrow = i < n;
+    const int ic = qrow ? i : n - 1;
+
+    // ------------------------------------------------------------------ 1. stage
+    // unconditional buffer loads (clamped offsets, values selected afterwards): one HBM trip
+    const long Bn = (long)a.B * n;
+    const int voff = (int)(8 * (b * n + ic));
+    const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
+    const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    double mrow[NQ]; // M is symmetric: lane i's row is its column, so the loads coalesce
+    {
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
+        const int moff = (int)(8 * (b * n * n + ic));
+#pragma unroll
+        for (int r = 0; r < NQ; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    }
+    double jc[6 * kCMax], jw[6];
+    {
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.Jc, Bn * nc * 6);
+        const int joff = (int)(8 * (b * nc * 6 * n + ic));
+#pragma unroll
+        for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = bload(Jrs, joff, 8 * (rr < 6 * nc ? rr : 6 * nc - 1) * n);
+        const __amdgpu_buffer_rsrc_t Wrs = rsrc(a.Jw, Bn * 6);
+        const int woff = (int)(8 * (b * 6 * n + ic));
+#pragma unroll
+        for (int r = 0; r < 6; ++r) jw[r] = bload(Wrs, woff, 8 * r * n);
+    }
+    constexpr int kPoseIt = (24 * (1 + kCMax) + 63) / 64;
+    double pv[kPoseIt];
+#pragma unroll
+    for (int it = 0; it < kPoseIt; ++it) {
+        int e = it * 64 + i;
+        e = e < 24 * (1 + nc) ? e : 24 * (1 + nc) - 1;
+        const int t = e / 24, c = e - t * 24;
+        if (t == 0) pv[it] = c < 12 ? a.pose_w[b * 12 + c] : a.pose_w_ref[b * 12 + c - 12];
+        else pv[it] = c < 12 ? a.pose_c[(b * nc + t - 1) * 12 + c] : a.pose_c_ref[(b * nc + t - 1) * 12 + c - 12];
+    }
+    double jd = 0.0;
+    if (i < 6 * (1 + nc)) jd = i < 6 ? a.jdqd_w[b * 6 + i] : a.jdqd_c[b * nc * 6 + i - 6];
+    const double h_i = qrow ? h_i0 : 0.0;
+#pragma unroll
+    for (int r = 0; r < NQ; ++r) mrow[r] = (qrow && r < n) ? mrow[r] : 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = (qrow && rr < 6 * nc) ? jc[rr] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) jw[r] = qrow ? jw[r] : 0.0;
+    if (qrow) {
+#pragma unroll
+        for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = mrow[r];
+#pragma unroll
+        for (int f = 0; f < 3 * kCMax; ++f)
+            if (f < nf) S[L.FFJ + i * L.FS + f] = ((cm >> (f / 3)) & 1) ? -jc[6 * (f / 3) + f % 3] : 0.0;
+    }
+    if (i < NQ) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) S[L.AQW + r * L.QS + i] = jw[r];
+#pragma unroll
+        for (int rr = 0; rr < 6 * kCMax; ++rr)
+            if (rr < 6 * nc) S[L.JC + rr * NQ + i] = jc[rr];
+    }
+    S[L.QD + i] = qrow ? qd_i : 0.0;
+#pragma unroll
+    for (int it = 0; it < kPoseIt; ++it)
+        if (it * 64 + i < 24 * (1 + nc)) S[L.PS + it * 64 + i] = pv[it];
+    if (i < 6 * (1 + nc)) S[L.JD + i] = jd;
+    __syncthreads();
+
+    // ------------------------------------------------- 2. task targets (one lane per row)
+    // Cartesian acceleration task: b = Kp e - Kd J qd - Jdot qd (xdd_ref = 0, xd_ref = 0)
+    if (i < 6 * (1 + nc)) {
+        const int t = i / 6, r = i - 6 * t;
+        const double *Jr = t == 0 ? S + L.AQW + r * L.QS : S + L.JC + (6 * (t - 1) + r) * NQ;
+        double xd = 0.0;
+        for (int j = 0; j < n; ++j) xd = fma(Jr[j], S[L.QD + j], xd);
+        const double e = cart_error_component(S + L.PS + 24 * t, S + L.PS + 24 * t + 12, r);
+        const double Kp = t == 0 ? a.Kp_w : a.Kp_f, Kd = t == 0 ? a.Kd_w : a.Kd_f;
+        S[L.BT + i] = Kp * e - Kd * xd - S[L.JD + i];
+    }
+    __syncthreads();
+
+    // ------------------------------- 3. H row i = e_i + sum_c J_c^T J_c row i, gradient
+    double A[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) A[j] = (j == i) ? 1.0 : 0.0;
+    double mg = qrow ? a.Kp_p * (qref_i - q_i) - a.Kd_p * qd_i : 0.0; // -g_i = b_p + sum J_c^T b_c
+#pragma unroll
+    for (int rr = 0; rr < 6 * kCMax; ++rr) {
+        if (rr < 6 * nc) {
+            const double v = jc[rr];
+            const double *Jr = S + L.JC + rr * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) A[j] = fma(v, Jr[j], A[j]);
+            mg = fma(v, S[L.BT + 6 + rr], mg);
+        }
+    }
+    if constexpr (NQ == 64 && TR) {
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) S[L.HR + i * L.QS + j] = A[j];
+    }
+
+    // ------------- 4. X = H_qq^-1 [M rows 0..NJ-1 | J_w^T | -g]: block Gauss-Jordan, H SPD
+    bool notspd = false;
+    for (int c0 = 0; c0 < L.NR; c0 += NRC) {
+        if constexpr (NQ == 64 && TR) {
+            if (c0 > 0) {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) A[j] = S[L.HR + i * L.QS + j];
+            }
+        }
+        double rhs[NRC];
+#pragma unroll
+        for (int m = 0; m < NRC; ++m) {
+            const int s = c0 + m;
+            double v = 0.0;
+            if (s < L.NJ) v = S[L.AQJ + ic * L.QS + s];
+            else if (s < L.NJ + 6) v = S[L.AQW + (s - L.NJ) * L.QS + (i < NQ ? i : 0)];
+            else if (s == L.NJ + 6) v = mg;
+            rhs[m] = qrow ? v : 0.0;
+        }
+        __syncthreads();
+        notspd |= block_gj<NQ, NRC, NRC>(A, rhs, n, i, S + L.PN, S + L.RH);
+        if (i < NQ) {
+#pragma unroll
+            for (int m = 0; m < NRC; ++m)
+                if (c0 + m < L.NR) S[L.XT + (c0 + m) * L.QS + i] = rhs[m];
+        }
+    }
+    __syncthreads();
+    {
+        const double x0 = qrow ? S[L.XT + (L.NJ + 6) * L.QS + i] : 0.0;
+        S[L.X0 + i] = x0;
+        S[L.XV + i] = x0;
+    }
+
+    // ------------------------------------------ 5. Gamma row ci, activities, bounds
+    const int ci = i;
+    const int NJ = L.NJ, ME = L.ME;
+    int kind = 0; // 0 disabled, 1 equality, 2 inequality (lo <= a x <= hi)
+    double lo = -kInf, hi = kInf;
+    if (ci < NJ) {
+        if (ci < 6) {
+            kind = 1;
+            lo = hi = -h_i; // M_fb qdd - J_fb^T f = -h_fb
+        } else {
+            kind = 2;
+            lo = a.tau_min[ci] - h_i;
+            hi = a.tau_max[ci] - h_i;
+        }
+    } else if (ci < NJ + 6) {
+        kind = 1;
+        lo = hi = S[L.BT + ci - NJ];
+    } else if (ci < ME) {
+        const int f = ci - NJ - 6, c = f / 3, k = f - 3 * c;
+        if ((cm >> c) & 1) {
+            kind = 2;
+            lo = a.f_lb[k];
+            hi = a.f_ub[k];
+        }
+    }
+    const double ieps = 1.0 / a.eps_f;
+    double s_i = 0.0, nrm = 1.0;
+    if (kind != 0) {
+        double aq[NQ], fc[3 * kCMax];
+        const double *rq = row_q(S, L, ci);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) aq[j] = rq ? rq[j] : 0.0;
+#pragma unroll
+        for (int f = 0; f < 3 * kCMax; ++f) fc[f] = f < nf ? fcoef(S, L, ci, f) : 0.0;
+        for (int cl = 0; cl < ME; ++cl) {
+            double g = 0.0;
+            if (cl < NJ + 6) {
+                const double *xt = S + L.XT + cl * L.QS;
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) g = fma(aq[j], xt[j], g);
+            }
+            double gf = 0.0;
+            if (cl < NJ) {
+                const double *fr = S + L.FFJ + cl * L.FS;
+#pragma unroll
+                for (int f = 0; f < 3 * kCMax; ++f)
+                    if (f < nf) gf = fma(fc[f], fr[f], gf);
+            } else if (cl >= NJ + 6) {
+                const int fl = cl - NJ - 6;
+#pragma unroll
+                for (int f = 0; f < 3 * kCMax; ++f)
+                    if (f == fl) gf = fc[f];
+            }
+            S[L.GM + ci * L.GS + cl] = fma(gf, ieps, g);
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) s_i = fma(aq[j], S[L.X0 + j], s_i);
+    }
+    __syncthreads();
+    if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
+    const bool cons_eq = kind == 1;
+
+    // ------------------------------------ 6. dual active set in constraint space
+    int status = notspd ? 3 : (a.limits_crossed ? 2 : 0);
+    int iters = 0, k = 0;
+    int act = 0;       // slot i < k: compact row
+    double sgn = 1.0;  // its sign (normal = sgn * a_act)
+    double lam = 0.0;  // its multiplier
+    bool aeq = false;  // it is an equality (never dropped)
+    bool onact = false; // lane ci: row ci is in the active set
+    int eqn = 0, rounds = 0;
+    bool need_select = true, dirty = true;
+    int cp = 0;
+    double sgp = 1.0, bnd = 0.0, lamp = 0.0;
+    const int maxit = a.max_iter;
+    bool go = status == 0;
+    while (go) {
+        if (need_select) {
+            if (eqn < 12) { // equalities first, in order: dynamics, then waist
+                cp = eqn < 6 ? eqn : NJ + eqn - 6;
+                ++eqn;
+                const double sp = __shfl(s_i, cp);
+                bnd = __shfl(lo, cp);
+                sgp = (sp - bnd > 0.0) ? -1.0 : 1.0;
+            } else {
+                double v = -1.0;
+                if (kind == 2 && !onact) {
+                    const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                    const double viol = fmax(lo - s_i, s_i - hi);
+                    if (viol > tol) v = viol / nrm;
+                }
+                int pi = i;
+                iargmax<64>(v, pi);
+                if (!(v > 0.0)) {
+                    // no violated row: x is current unless steps were taken since the last
+                    // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on
+                    // the active set, and re-check every row with the exact activities
+                    if (!dirty || rounds >= 3) break;
+                    ++rounds;
+                    dirty = false;
+                    rebuild_refine(S, L, i, k, n, nf, act, sgn, lam, lo, hi, ieps);
+                    if (kind != 0) s_i = activity(S, L, ci, n, nf);
+                    continue;
+                }
+                cp = pi;
+                const double vl = __shfl(lo - s_i, cp), vh = __shfl(s_i - hi, cp);
+                sgp = vl > vh ? 1.0 : -1.0;
+                bnd = sgp > 0.0 ? __shfl(lo, cp) : __shfl(hi, cp);
+            }
+            lamp = 0.0;
+        }
+        if (++iters > maxit) {
+            status = 1;
+            break;
+        }
+        dirty = true;
+        // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
+        const double gpp = S[L.GM + cp * L.GS + cp];
+        if (i < k) S[L.VV + i] = sgn * sgp * S[L.GM + act * L.GS + cp];
+        __syncthreads();
+        double l = 0.0;
+        if (i < k)
+            for (int q = 0; q <= i; ++q) l = fma(S[L.TT + i * L.TS + q], S[L.VV + q], l);
+        S[L.LV + i] = l;
+        __syncthreads();
+        double r = 0.0;
+        if (i < k)
+            for (int q = i; q < k; ++q) r = fma(S[L.TT + q * L.TS + i], S[L.LV + q], r);
+        const double d2 = gpp - isum<64>(l * l);
+        S[L.RV + i] = i < k ? sgn * r : 0.0;
+        S[L.AC + i] = (double)act;
+        __syncthreads();
+        double ds = 0.0;
+        if (kind != 0) {
+            const double *gr = S + L.GM + ci * L.GS;
+            ds = sgp * gr[cp];
+            for (int q = 0; q < k; ++q) ds = fma(-gr[(int)S[L.AC + q]], S[L.RV + q], ds);
+        }
+        const double zz = sgp * __shfl(ds, cp);
+        const double slack = sgp * (__shfl(s_i, cp) - bnd); // < 0: violated
+        const double rmax = imax<64>(i < k ? fabs(r) : 0.0);
+        double cand = (i < k && !aeq && r > 1e-13 * rmax) ? lam / r : kInf;
+        int blk = i;
+        iargmin<64>(cand, blk);
+        const double t1 = cand;
+        const double t2 = (zz > 1e-14 * gpp) ? -slack / zz : kInf;
+        const bool peq = __shfl(cons_eq ? 1 : 0, cp) != 0;
+        if (t1 >= kInf && t2 >= kInf) {
+            if (peq && fabs(slack) <= 1e-10 * fmax(1.0, fabs(bnd))) { // dependent, consistent
+                need_select = true;
+                __syncthreads();
+                continue;
+            }
+            status = 2; // no feasible point with level 0 at b_w (level-0 repair: next)
+            break;
+        }
+        const double t = fmin(t1, t2);
+        s_i = fma(t, ds, s_i);
+        if (i < k) lam = fma(-t, r, lam);
+        lamp += t;
+        if (t2 <= t1) { // add cp
+            const double dd = d2 > 0.0 ? d2 : zz;
+            const double id = frsq(dd);
+            if (i < k) S[L.TT + k * L.TS + i] = -r * id;
+            if (i == k) {
+                S[L.TT + k * L.TS + k] = id;
+                act = cp;
+                sgn = sgp;
+                lam = lamp;
+                aeq = peq;
+            }
+            if (i == cp) onact = true;
+            ++k;
+            need_select = true;
+            __syncthreads();
+        } else { // drop slot blk (its multiplier reached zero), keep stepping on cp
+            const int cb = __shfl(act, blk);
+            if (i == cb) onact = false;
+            const int na = __shfl(act, i + 1);
+            const double ns = __shfl(sgn, i + 1), nl = __shfl(lam, i + 1);
+            const bool ne = __shfl(aeq ? 1 : 0, i + 1) != 0;
+            if (i >= blk) {
+                act = na;
+                sgn = ns;
+                lam = nl;
+                aeq = ne;
+            }
+            --k;
+            __syncthreads();
+            for (int a2 = blk; a2 < k; ++a2) // rows before blk of T stand; re-append the rest
+                (void)t_append(S, L, i, a2, __shfl(act, a2), __shfl(sgn, a2), act, sgn);
+            need_select = false;
+        }
+    }
+
+    // ------------------------------------------------------------------ 7. outputs
+    __syncthreads();
+    const bool ok = status == 0;
+    double tau_i = h_i;
+    if (ok && qrow) { // joint row i: M_i qdd - J_c,i^T f + h_i
+        double t = h_i;
+        for (int j = 0; j < n; ++j) t = fma(S[L.AQJ + i * L.QS + j], S[L.XV + j], t);
+        for (int f = 0; f < nf; ++f) t = fma(S[L.FFJ + i * L.FS + f], S[L.XV + n + f], t);
+        tau_i = t;
+    }
+    const double tmax = imax<64>((qrow && !isfinite(tau_i)) ? 1.0 : 0.0);
+    if (ok && tmax > 0.0) status = 3;
+    if (status != 0) tau_i = h_i;
+    if (qrow) a.tau[b * n + i] = tau_i;
+    if (i < L.NX) a.x[b * L.NX + i] = status == 0 ? S[L.XV + i] : 0.0;
+    if (i == 0) {
+        a.status[b] = status;
+        a.iters[b] = iters;
+    }
+}
+
+template <int NQ, bool TR>
+hipError_t launch_t(const ContactArgs &a, hipStream_t stream)
+{
+    constexpr int NRC = TR ? 40 : 16;
+    static size_t attr = 0;
+    const ContactLayout L(a.n, a.nc, TR, NQ, NRC);
+    if (L.NR > NRC * ((NQ == 64 && TR) ? 2 : 1) || L.ME > 64 || L.NX > 64) return hipErrorInvalidValue;
+    const size_t lds = sizeof(double) * L.SIZE;
+    if (lds > attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)contact_kernel<NQ, TR>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = lds;
+    }
+    hipLaunchKernelGGL((contact_kernel<NQ, TR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t contact_lds_bytes(int n, int nc, int torque_rows)
+{
+    const bool tr = torque_rows != 0;
+    const int NQ = n <= 32 ? 32 : 64;
+    return sizeof(double) * ContactLayout(n, nc, tr, NQ, tr ? 40 : 16).SIZE;
+}
+
+hipError_t launch_contact(const ContactArgs &a, hipStream_t stream)
+{
+    if (a.B <= 0) return hipSuccess;
+    if (a.n <= 32) return a.torque_rows ? launch_t<32, true>(a, stream) : launch_t<32, false>(a, stream);
+    return a.torque_rows ? launch_t<64, true>(a, stream) : launch_t<64, false>(a, stream);
+}
+
+}  // namespace wbq

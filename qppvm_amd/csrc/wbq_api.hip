@@ -16,7 +16,11 @@
 
 struct wbq_ctx {
     int device = 0;
-    wbq_desc d{};
+    int form = WBQ_FORM_QPPVM;
+    wbq_desc d{};              // QPPVM form (d.n, d.max_batch, d.max_iter are set for both forms)
+    wbq_contact_desc cd{};     // contact form
+    int nfield = 0;            // fp64 input fields and their elements per instance
+    size_t fe[16] = {};
     int m0 = 0;
     int limits_crossed = 0;
     hipStream_t own_stream = nullptr;
@@ -29,7 +33,10 @@ struct wbq_ctx {
     double *dev_in = nullptr, *host_in = nullptr;
     hipEvent_t in_copied = nullptr;
     bool in_pending = false;
-    const double *in[8] = {};
+    const double *in[16] = {};
+    const int *cmask = nullptr; // contact form: [B] (packed after the fp64 fields when staged)
+    double *dev_x = nullptr;     // contact form: x [max_batch][nx]
+    int nx = 0;
     int batch = 0;
     bool have_inputs = false;
     // outputs: one device block [tau | status | iters] packed for the current batch (single
@@ -60,7 +67,7 @@ struct wbq_ctx {
 
 namespace {
 
-const char *kVersion = "wbq 0.1.0 (gfx950, fp64, QPPVM form)";
+const char *kVersion = "wbq 0.2.0 (gfx950, fp64, QPPVM + contact forms)";
 
 size_t field_elems(const wbq_desc &d, int f)
 {
@@ -71,6 +78,23 @@ size_t field_elems(const wbq_desc &d, int f)
     case 2: return T * 12;     // pose
     case 3: return T * 12;     // pose_ref
     default: return n;         // q, qd, qref, h
+    }
+}
+
+// contact form fields: M, h, q, qd, qref, Jw, jdqd_w, pose_w, pose_w_ref, Jc, jdqd_c, pose_c, pose_c_ref
+constexpr int kContactFields = 13;
+size_t contact_field_elems(const wbq_contact_desc &d, int f)
+{
+    const size_t n = (size_t)d.n, nc = (size_t)d.nc;
+    switch (f) {
+    case 0: return n * n;
+    case 1: case 2: case 3: case 4: return n;
+    case 5: return 6 * n;
+    case 6: return 6;
+    case 7: case 8: return 12;
+    case 9: return nc * 6 * n;
+    case 10: return nc * 6;
+    default: return nc * 12; // 11, 12
     }
 }
 
@@ -90,6 +114,58 @@ int hip_fail(wbq_ctx *c, hipError_t e, const char *what)
         hipError_t e_ = (call);                         \
         if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
     } while (0)
+
+int solve_contact(wbq_ctx *c)
+{
+    const wbq_contact_desc &d = c->cd;
+    wbq::ContactArgs a{};
+    a.B = c->batch;
+    a.n = d.n;
+    a.nc = d.nc;
+    a.torque_rows = d.torque_rows;
+    a.max_iter = d.max_iter;
+    a.limits_crossed = c->limits_crossed;
+    a.Kp_w = d.Kp_w;
+    a.Kd_w = d.Kd_w;
+    a.Kp_f = d.Kp_f;
+    a.Kd_f = d.Kd_f;
+    a.Kp_p = d.Kp_p;
+    a.Kd_p = d.Kd_p;
+    a.eps_f = d.eps_f;
+    for (int k = 0; k < 3; ++k) {
+        a.f_lb[k] = d.f_lb[k];
+        a.f_ub[k] = d.f_ub[k];
+    }
+    a.tau_max = c->tmax;
+    a.tau_min = c->tmin;
+    a.M = c->in[0];
+    a.h = c->in[1];
+    a.q = c->in[2];
+    a.qd = c->in[3];
+    a.qref = c->in[4];
+    a.Jw = c->in[5];
+    a.jdqd_w = c->in[6];
+    a.pose_w = c->in[7];
+    a.pose_w_ref = c->in[8];
+    a.Jc = c->in[9];
+    a.jdqd_c = c->in[10];
+    a.pose_c = c->in[11];
+    a.pose_c_ref = c->in[12];
+    a.cmask = c->cmask;
+    a.tau = c->out_tau ? c->out_tau : c->tau;
+    a.status = c->out_status ? c->out_status : c->status;
+    a.iters = c->out_iters ? c->out_iters : c->iters;
+    a.x = c->dev_x;
+    WBQ_HIP(hipSetDevice(c->device));
+    const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
+    if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
+    WBQ_HIP(wbq::launch_contact(a, c->stream));
+    if (timed) {
+        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+        c->ev_used += 2;
+    }
+    return WBQ_SUCCESS;
+}
 
 }  // namespace
 
@@ -140,8 +216,10 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
               hipMalloc(&c->Kq, n * 8) == hipSuccess && hipMalloc(&c->Dq, n * 8) == hipSuccess &&
               hipMalloc(&c->tmax, n * 8) == hipSuccess && hipMalloc(&c->tmin, n * 8) == hipSuccess &&
               hipMalloc(&c->row_sel, sizeof(int) * wbq::kM0Max) == hipSuccess;
+    c->nfield = 8;
+    for (int f = 0; f < 8; ++f) c->fe[f] = field_elems(d, f);
     size_t in_elems = 0;
-    for (int f = 0; f < 8; ++f) in_elems += field_elems(d, f) * B;
+    for (int f = 0; f < 8; ++f) in_elems += c->fe[f] * B;
     const size_t out_bytes = n * B * 8 + 2 * B * 4 + 16;
     ok = ok && hipMalloc(&c->dev_in, in_elems * 8) == hipSuccess &&
          hipHostMalloc((void **)&c->host_in, in_elems * 8, hipHostMallocDefault) == hipSuccess &&
@@ -177,6 +255,122 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     return WBQ_SUCCESS;
 }
 
+int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
+{
+    if (!out || !desc) return WBQ_E_INVALID;
+    *out = nullptr;
+    const wbq_contact_desc &d = *desc;
+    if (d.n_fb != 6 || d.n <= 6 || d.nc < 1 || d.nc > wbq::kCMax || d.max_batch < 1) return WBQ_E_INVALID;
+    if (d.n + 3 * d.nc > 64 || (d.torque_rows ? d.n : 6) + 6 + 3 * d.nc > 64) return WBQ_E_UNSUPPORTED;
+    if (!(d.eps_f > 0.0)) return WBQ_E_INVALID;
+    if (d.torque_rows && (!d.tau_max || !d.tau_min)) return WBQ_E_INVALID;
+    for (int k = 0; k < 3; ++k)
+        if (!(d.f_lb[k] <= d.f_ub[k])) return WBQ_E_INVALID;
+    wbq_ctx *c = new wbq_ctx();
+    c->form = WBQ_FORM_CONTACT;
+    c->cd = d;
+    c->cd.tau_max = c->cd.tau_min = nullptr;
+    c->nx = d.n + 3 * d.nc;
+    const int me = (d.torque_rows ? d.n : 6) + 6 + 3 * d.nc;
+    if (c->cd.max_iter <= 0) c->cd.max_iter = 10 * (c->nx + me) + 50;
+    c->d.n = d.n;
+    c->d.max_batch = d.max_batch;
+    c->d.max_iter = c->cd.max_iter;
+    c->device = device;
+    if (d.torque_rows)
+        for (int j = d.n_fb; j < d.n; ++j)
+            if (d.tau_min[j] > d.tau_max[j]) c->limits_crossed = 1;
+    auto cleanup = [&](int rc) {
+        wbq_destroy(c);
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(WBQ_E_DEVICE);
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(WBQ_E_DEVICE);
+    c->stream = c->own_stream;
+    const size_t n = (size_t)d.n, B = (size_t)d.max_batch;
+    c->nfield = kContactFields;
+    size_t in_elems = 0;
+    for (int f = 0; f < kContactFields; ++f) {
+        c->fe[f] = contact_field_elems(d, f);
+        in_elems += c->fe[f] * B;
+    }
+    const size_t cm_elems = (B + 1) / 2; // the int32 contact masks, packed after the fp64 fields
+    const size_t out_bytes = n * B * 8 + 2 * B * 4 + 16;
+    std::vector<double> tmx(n, 0.0), tmn(n, 0.0);
+    if (d.torque_rows) {
+        std::memcpy(tmx.data(), d.tau_max, n * 8);
+        std::memcpy(tmn.data(), d.tau_min, n * 8);
+    }
+    bool ok = hipMalloc(&c->tmax, n * 8) == hipSuccess && hipMalloc(&c->tmin, n * 8) == hipSuccess &&
+              hipMalloc(&c->dev_in, (in_elems + cm_elems) * 8) == hipSuccess &&
+              hipHostMalloc((void **)&c->host_in, (in_elems + cm_elems) * 8, hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&c->dev_out, out_bytes) == hipSuccess &&
+              hipHostMalloc((void **)&c->host_out, out_bytes, hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&c->dev_x, B * c->nx * 8) == hipSuccess &&
+              hipEventCreateWithFlags(&c->in_copied, hipEventDisableTiming) == hipSuccess;
+    if (!ok) return cleanup(WBQ_E_DEVICE);
+    ok = hipMemcpy(c->tmax, tmx.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(c->tmin, tmn.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) return cleanup(WBQ_E_DEVICE);
+    *out = c;
+    return WBQ_SUCCESS;
+}
+
+int wbq_set_contact_inputs(wbq_ctx *c, const wbq_contact_inputs *in)
+{
+    if (!c || !in) return WBQ_E_INVALID;
+    if (c->form != WBQ_FORM_CONTACT) return fail(c, WBQ_E_INVALID, "wbq_set_contact_inputs on a QPPVM-form context");
+    if (in->batch < 0 || in->batch > c->d.max_batch) return fail(c, WBQ_E_CAPACITY, "batch exceeds max_batch");
+    const double *src[kContactFields] = {in->M, in->h, in->q, in->qd, in->qref, in->Jw, in->jdqd_w, in->pose_w,
+                                         in->pose_w_ref, in->Jc, in->jdqd_c, in->pose_c, in->pose_c_ref};
+    if (in->batch > 0) {
+        for (int f = 0; f < kContactFields; ++f)
+            if (!src[f]) return fail(c, WBQ_E_INVALID, "null input pointer");
+        if (!in->cmask) return fail(c, WBQ_E_INVALID, "null contact mask");
+    }
+    if (in->memory != WBQ_MEM_DEVICE && in->memory != WBQ_MEM_HOST)
+        return fail(c, WBQ_E_INVALID, "unknown memory kind");
+    WBQ_HIP(hipSetDevice(c->device));
+    if (in->memory == WBQ_MEM_DEVICE) {
+        for (int f = 0; f < kContactFields; ++f) c->in[f] = src[f];
+        c->cmask = in->cmask;
+    } else {
+        if (c->in_pending) WBQ_HIP(hipEventSynchronize(c->in_copied));
+        size_t off = 0;
+        for (int f = 0; f < kContactFields; ++f) {
+            const size_t e = c->fe[f] * (size_t)in->batch;
+            if (e) std::memcpy(c->host_in + off, src[f], e * 8);
+            c->in[f] = c->dev_in + off;
+            off += e;
+        }
+        if (in->batch > 0) std::memcpy(c->host_in + off, in->cmask, (size_t)in->batch * 4);
+        c->cmask = (const int *)(c->dev_in + off);
+        off += ((size_t)in->batch + 1) / 2;
+        if (in->batch > 0) {
+            WBQ_HIP(hipMemcpyAsync(c->dev_in, c->host_in, off * 8, hipMemcpyHostToDevice, c->stream));
+            WBQ_HIP(hipEventRecord(c->in_copied, c->stream));
+            c->in_pending = true;
+        }
+    }
+    c->batch = in->batch;
+    c->tau = c->dev_out;
+    c->status = (int *)(c->dev_out + (size_t)c->batch * c->d.n);
+    c->iters = c->status + c->batch;
+    c->have_inputs = true;
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_contact_outputs(wbq_ctx *c, double *x)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (c->form != WBQ_FORM_CONTACT) return fail(c, WBQ_E_INVALID, "not a contact-form context");
+    if (!x || c->batch == 0) return WBQ_SUCCESS;
+    WBQ_HIP(hipSetDevice(c->device));
+    WBQ_HIP(hipMemcpyAsync(x, c->dev_x, (size_t)c->batch * c->nx * 8, hipMemcpyDeviceToHost, c->stream));
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    return WBQ_SUCCESS;
+}
+
 int wbq_set_stream(wbq_ctx *c, void *hip_stream)
 {
     if (!c) return WBQ_E_INVALID;
@@ -187,6 +381,7 @@ int wbq_set_stream(wbq_ctx *c, void *hip_stream)
 int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
 {
     if (!c || !in) return WBQ_E_INVALID;
+    if (c->form != WBQ_FORM_QPPVM) return fail(c, WBQ_E_INVALID, "wbq_set_inputs on a contact-form context");
     if (in->batch < 0 || in->batch > c->d.max_batch)
         return fail(c, WBQ_E_CAPACITY, "batch exceeds max_batch");
     const double *src[8] = {in->M, in->J, in->pose, in->pose_ref, in->q, in->qd, in->qref, in->h};
@@ -202,7 +397,7 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
         if (c->in_pending) WBQ_HIP(hipEventSynchronize(c->in_copied));
         size_t off = 0;
         for (int f = 0; f < 8; ++f) {
-            const size_t e = field_elems(c->d, f) * (size_t)in->batch;
+            const size_t e = c->fe[f] * (size_t)in->batch;
             if (e) std::memcpy(c->host_in + off, src[f], e * 8);
             c->in[f] = c->dev_in + off;
             off += e;
@@ -226,6 +421,7 @@ int wbq_solve(wbq_ctx *c)
 {
     if (!c) return WBQ_E_INVALID;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "wbq_set_inputs not called");
+    if (c->form == WBQ_FORM_CONTACT) return solve_contact(c);
     wbq::QppvmArgs a{};
     a.B = c->batch;
     a.n = c->d.n;
@@ -328,6 +524,7 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
     // Drops the per-instance warm start (repair hint + BVLS bound state), stream-ordered
     // with the solves; a cold instance takes the default path next time.
     if (!c) return WBQ_E_INVALID;
+    if (!c->ws_hint) return WBQ_SUCCESS; // no warm-start state in this form
     WBQ_HIP(hipSetDevice(c->device));
     const int B = c->d.max_batch;
     int b = 0;
@@ -412,6 +609,7 @@ void wbq_destroy(wbq_ctx *c)
     if (c->work) (void)hipFree(c->work);
     if (c->ws_hint) (void)hipFree(c->ws_hint);
     if (c->ws_state) (void)hipFree(c->ws_state);
+    if (c->dev_x) (void)hipFree(c->dev_x);
 
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;

@@ -1,0 +1,294 @@
+// wbq_device.h -- device helpers shared by the QPPVM and contact-form kernels (gfx950, fp64).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+namespace wbq {
+
+constexpr double kInf = 1.0e300;
+
+// fast reciprocal / reciprocal square root: hardware estimate + one Newton step (~0.5 ulp)
+__device__ __forceinline__ double frcp(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double frsq(double x)
+{
+    double y = __builtin_amdgcn_rsq(x);
+    return y * fma(-0.5 * x * y, y, 1.5);
+}
+
+// Raw buffer loads: one 32-bit per-lane byte offset + a uniform SGPR offset per load, so an
+// unrolled run of loads costs no address VGPRs (a flat load would need a 64-bit address each).
+// Out-of-range offsets read 0 (hardware bounds check on num_records).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double *p, long elems)
+{
+    const long bytes = elems * 8;
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                             0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff_bytes, soff_bytes, 0));
+}
+
+// One row of an NP-column matrix per lane: in VGPRs (compile-time indices, runtime
+// writes by select) or in LDS.
+template <int NP, bool REG>
+struct RowStore;
+
+template <int NP>
+struct RowStore<NP, true> {
+    double v[NP];
+    __device__ void bind(double *) {}
+    __device__ void zero()
+    {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) v[j] = 0.0;
+    }
+    __device__ void set(int c, double x)
+    {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) v[j] = (j == c) ? x : v[j];
+    }
+    __device__ double get(int c) const
+    {
+        double r = 0.0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) r = (j == c) ? v[j] : r;
+        return r;
+    }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+            if (j < cnt) s = fma(v[j], b[j], s);
+        return s;
+    }
+};
+
+template <int NP>
+struct RowStore<NP, false> {
+    double *row;
+    __device__ void bind(double *p) { row = p; }
+    __device__ void zero()
+    {
+        for (int j = 0; j < NP; ++j) row[j] = 0.0;
+    }
+    __device__ void set(int c, double x) { row[c] = x; }
+    __device__ double get(int c) const { return row[c]; }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int j = 0; j < cnt; ++j) s = fma(row[j], b[j], s);
+        return s;
+    }
+};
+
+template <int NP>
+__device__ __forceinline__ double isum(double v)
+{
+#pragma unroll
+    for (int m = NP / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, NP);
+    return v;
+}
+
+template <int NP>
+__device__ __forceinline__ double imax(double v)
+{
+#pragma unroll
+    for (int m = NP / 2; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, NP));
+    return v;
+}
+
+// (value, index) reductions inside an instance; ties -> lowest index
+template <int NP>
+__device__ __forceinline__ void iargmax(double &v, int &idx)
+{
+#pragma unroll
+    for (int m = NP / 2; m >= 1; m >>= 1) {
+        const double ov = __shfl_xor(v, m, NP);
+        const int oi = __shfl_xor(idx, m, NP);
+        if (ov > v || (ov == v && oi < idx)) {
+            v = ov;
+            idx = oi;
+        }
+    }
+}
+
+template <int NP>
+__device__ __forceinline__ void iargmin(double &v, int &idx)
+{
+#pragma unroll
+    for (int m = NP / 2; m >= 1; m >>= 1) {
+        const double ov = __shfl_xor(v, m, NP);
+        const int oi = __shfl_xor(idx, m, NP);
+        if (ov < v || (ov == v && oi < idx)) {
+            v = ov;
+            idx = oi;
+        }
+    }
+}
+
+// Cartesian error component r of e = [p_ref - p ; vec(quat(R_ref R^T)), w >= 0]
+// (same specification as oracle/wbq_oracle.c:wbq_ref_cart_error).
+__device__ double cart_error_component(const double *P, const double *Pr, int r)
+{
+    if (r < 3) return Pr[4 * r + 3] - P[4 * r + 3];
+    double Re[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            Re[3 * a + c] = Pr[4 * a] * P[4 * c] + Pr[4 * a + 1] * P[4 * c + 1] + Pr[4 * a + 2] * P[4 * c + 2];
+    const double tr = Re[0] + Re[4] + Re[8];
+    double qw, qx, qy, qz;
+    if (tr > 0.0) {
+        const double s = sqrt(tr + 1.0) * 2.0;
+        qw = 0.25 * s;
+        qx = (Re[7] - Re[5]) / s;
+        qy = (Re[2] - Re[6]) / s;
+        qz = (Re[3] - Re[1]) / s;
+    } else if (Re[0] > Re[4] && Re[0] > Re[8]) {
+        const double s = sqrt(1.0 + Re[0] - Re[4] - Re[8]) * 2.0;
+        qw = (Re[7] - Re[5]) / s;
+        qx = 0.25 * s;
+        qy = (Re[1] + Re[3]) / s;
+        qz = (Re[2] + Re[6]) / s;
+    } else if (Re[4] > Re[8]) {
+        const double s = sqrt(1.0 + Re[4] - Re[0] - Re[8]) * 2.0;
+        qw = (Re[2] - Re[6]) / s;
+        qx = (Re[1] + Re[3]) / s;
+        qy = 0.25 * s;
+        qz = (Re[5] + Re[7]) / s;
+    } else {
+        const double s = sqrt(1.0 + Re[8] - Re[0] - Re[4]) * 2.0;
+        qw = (Re[3] - Re[1]) / s;
+        qx = (Re[2] + Re[6]) / s;
+        qy = (Re[5] + Re[7]) / s;
+        qz = 0.25 * s;
+    }
+    const double sg = (qw < 0.0) ? -1.0 : 1.0;
+    return sg * (r == 3 ? qx : (r == 4 ? qy : qz));
+}
+
+// In-place block Gauss-Jordan on an SPD matrix held one row per lane (A = row i), with NR
+// right-hand sides per row; returns true if a pivot was not positive (M not SPD). On exit
+// rhs = M^-1 rhs (row i). PN: LDS [2][NP][4] panel, RH: LDS [2][4][RHS] pivot-row rhs.
+//
+// Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing Schur
+// complement stays symmetric: pivot row k+r, column j, equals lane j's entry in column k+r.
+// Every lane publishes its BS panel entries; every lane factors the BS x BS pivot block D
+// redundantly and applies one rank-BS update:
+//   rows outside the block: row -= (a_i D^-1) P,   rows inside: row = (D^-1)_ri P,
+// so each row ends up normalised by its own pivot block (x_i = rhs_i, no division).
+// The next panel is updated and published first (lookahead), then the rest of the row.
+template <int NP, int NR, int RHS>
+__device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int n, int i, double *PN, double *RH)
+{
+    constexpr int BS = 4;
+    bool notspd = false;
+    if (i < NP) {
+#pragma unroll
+        for (int c = 0; c < BS; ++c) PN[i * BS + c] = A[c];
+    }
+    if (i < BS) {
+#pragma unroll
+        for (int m = 0; m < NR; ++m) RH[i * RHS + m] = rhs[m];
+    }
+#pragma unroll
+    for (int kb = 0; kb < NP / BS; ++kb) {
+        const int k = kb * BS;
+        if (k < n) {
+            __syncthreads();
+            const double *pn = PN + (kb & 1) * NP * BS;
+            const double *rh = RH + (kb & 1) * BS * RHS;
+            double *pnn = PN + ((kb + 1) & 1) * NP * BS;
+            double *rhn = RH + ((kb + 1) & 1) * BS * RHS;
+            // Cholesky of the pivot block (redundant per lane)
+            double d[BS][BS];
+#pragma unroll
+            for (int r = 0; r < BS; ++r)
+#pragma unroll
+                for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
+            double il[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double dd = d[c][c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
+                notspd |= !(dd > 0.0);
+                il[c] = frsq(dd);
+#pragma unroll
+                for (int r = c + 1; r < BS; ++r) {
+                    double t = d[r][c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
+                    d[r][c] = t * il[c];
+                }
+            }
+            // solve D y = e, e = unit(i-k) for the block's own rows, else a_i = row i's panel
+            const int ri = i - k;
+            const bool inK = ri >= 0 && ri < BS;
+            double y[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double v = inK ? (ri == c ? 1.0 : 0.0) : A[k + c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
+                y[c] = v * il[c];
+            }
+#pragma unroll
+            for (int c = BS - 1; c >= 0; --c) {
+                double v = y[c];
+#pragma unroll
+                for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
+                y[c] = v * il[c];
+            }
+            const double cc = inK ? 0.0 : 1.0;
+            double hh[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) hh[c] = inK ? y[c] : -y[c];
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                double v = cc * rhs[m];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], rh[c * RHS + m], v);
+                rhs[m] = v;
+            }
+            // lookahead: next panel first
+#pragma unroll
+            for (int j = k + BS; j < k + 2 * BS && j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
+            if (k + BS < n) {
+                if (i < NP) {
+#pragma unroll
+                    for (int c = 0; c < BS; ++c)
+                        if (k + BS + c < NP) pnn[i * BS + c] = A[(k + BS + c) < NP ? k + BS + c : NP - 1];
+                }
+                const int rn = i - (k + BS);
+                if (rn >= 0 && rn < BS) {
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) rhn[rn * RHS + m] = rhs[m];
+                }
+            }
+#pragma unroll
+            for (int j = k + 2 * BS; j < NP; ++j) {
+                double v = cc * A[j];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                A[j] = v;
+            }
+        }
+    }
+    return notspd;
+}
+
+}  // namespace wbq

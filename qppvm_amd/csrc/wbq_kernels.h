@@ -52,6 +52,34 @@ constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream);
 
+// ------------------------------------------------------------------ contact form (ForceAcc)
+constexpr int kCMax = 4; // contacts
+
+// One launch of the contact-form solve (reference
+// src/ForceAcc.cpp:58-137,181-219). x = [qdd (n); f (3 per contact)].
+struct ContactArgs {
+    int B;           // instances
+    int n;           // DoF incl. the 6 floating-base coordinates (first)
+    int nc;          // contacts
+    int torque_rows; // a12 extension: actuated torque-limit rows
+    int max_iter;    // active-set step cap
+    int limits_crossed;
+    double Kp_w, Kd_w, Kp_f, Kd_f, Kp_p, Kd_p; // waist / feet / postural acceleration-task gains
+    double eps_f;                              // min-norm tie-break on the forces
+    double f_lb[3], f_ub[3];                   // force box of an active contact
+    const double *tau_max, *tau_min;           // [n] (device)
+    const double *M, *h, *q, *qd, *qref;       // [B][n][n], [B][n] x4
+    const double *Jw, *jdqd_w, *pose_w, *pose_w_ref; // [B][6][n], [B][6], [B][12] x2
+    const double *Jc, *jdqd_c, *pose_c, *pose_c_ref; // [B][nc][6][n], [B][nc][6], [B][nc][12] x2
+    const int *cmask;                          // [B] bit c = contact c active
+    double *tau;     // [B][n]
+    double *x;       // [B][n + 3 nc]
+    int *status;     // [B]
+    int *iters;      // [B]
+};
+
+hipError_t launch_contact(const ContactArgs &a, hipStream_t stream);
+
 // Lanes per instance used for a given n (32 for n <= 32, else 64).
 inline int lanes_per_instance(int n) { return n <= 32 ? 32 : 64; }
 

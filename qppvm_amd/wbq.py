@@ -10,19 +10,21 @@ import os
 
 import numpy as np
 
-from .problem import INPUT_FIELDS, QPPVMProblem, check_inputs
+from .problem import (CONTACT_INPUT_FIELDS, INPUT_FIELDS, ContactProblem, QPPVMProblem,
+                      check_contact_inputs, check_inputs)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libwbq.so")
 
 SUCCESS, E_INVALID, E_DEVICE, E_UNSUPPORTED, E_CAPACITY = 0, -1, -2, -3, -4
 MEM_HOST, MEM_DEVICE = 0, 1
-FORM_QPPVM = 0
+FORM_QPPVM, FORM_CONTACT = 0, 1
 
 # every symbol include/wbq.h declares (checked by tests/test_abi.py)
 EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
            "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
-           "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version")
+           "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
+           "wbq_set_contact_inputs", "wbq_get_contact_outputs")
 
 
 class WbqError(RuntimeError):
@@ -41,6 +43,22 @@ class Desc(ctypes.Structure):
 class Inputs(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int), ("memory", ctypes.c_int)] + \
                [(k, ctypes.c_void_p) for k in INPUT_FIELDS]
+
+
+class ContactDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("n_fb", ctypes.c_int), ("nc", ctypes.c_int),
+                ("torque_rows", ctypes.c_int), ("max_batch", ctypes.c_int), ("max_iter", ctypes.c_int)] + \
+               [(k, ctypes.c_double) for k in ("Kp_w", "Kd_w", "Kp_f", "Kd_f", "Kp_p", "Kd_p")] + \
+               [("f_lb", ctypes.c_double * 3), ("f_ub", ctypes.c_double * 3), ("eps_f", ctypes.c_double),
+                ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+
+
+_CONTACT_F64 = tuple(k for k in CONTACT_INPUT_FIELDS if k != "cmask")
+
+
+class ContactInputs(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int), ("memory", ctypes.c_int)] + \
+               [(k, ctypes.c_void_p) for k in _CONTACT_F64] + [("cmask", ctypes.c_void_p)]
 
 
 _lib = None
@@ -71,10 +89,13 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_last_error.argtypes = [P]
     lib.wbq_last_error.restype = ctypes.c_char_p
     lib.wbq_version.restype = ctypes.c_char_p
+    lib.wbq_create_contact.argtypes = [ctypes.POINTER(ContactDesc), I, ctypes.POINTER(P)]
+    lib.wbq_set_contact_inputs.argtypes = [P, ctypes.POINTER(ContactInputs)]
+    lib.wbq_get_contact_outputs.argtypes = [P, P]
     for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
               "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
-              "wbq_reset_warmstart",
-              "wbq_set_timing", "wbq_get_timing"):
+              "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
+              "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib
@@ -194,6 +215,54 @@ class QPPVMSolver:
         self._check(self.lib.wbq_get_timing(self.ctx, ctypes.byref(ms), ctypes.byref(cnt)),
                     "wbq_get_timing")
         return ms.value, cnt.value
+
+
+class ContactSolver(QPPVMSolver):
+    """Batched drop-in for ForceAccExample's per-tick solve (OptvarHelper variables, feet /
+    postural / waist acceleration tasks, DynamicFeasibility, wrench bounds, QPOases_sot, and
+    the inverse-dynamics post-step; reference src/ForceAcc.cpp:31-141,181-219).
+    Same context semantics as QPPVMSolver; outputs add x = [qdd; f]."""
+
+    def __init__(self, prob: ContactProblem, max_batch: int, device: int = 0):
+        self.lib = load_library()
+        self.prob = prob
+        self.max_batch = int(max_batch)
+        d = ContactDesc()
+        d.n, d.n_fb, d.nc, d.torque_rows = prob.n, prob.n_fb, prob.nc, int(bool(prob.torque_rows))
+        d.max_batch, d.max_iter = self.max_batch, int(prob.max_iter)
+        for k in ("Kp_w", "Kd_w", "Kp_f", "Kd_f", "Kp_p", "Kd_p", "eps_f"):
+            setattr(d, k, float(getattr(prob, k)))
+        for k in range(3):
+            d.f_lb[k], d.f_ub[k] = prob.f_lb[k], prob.f_ub[k]
+        self._keep = [np.ascontiguousarray(prob.tau_max, dtype=np.float64),
+                      np.ascontiguousarray(prob.tau_min, dtype=np.float64)]
+        d.tau_max, d.tau_min = _ptr(self._keep[0]), _ptr(self._keep[1])
+        h = ctypes.c_void_p()
+        rc = self.lib.wbq_create_contact(ctypes.byref(d), int(device), ctypes.byref(h))
+        if rc != SUCCESS:
+            raise WbqError(f"wbq_create_contact failed ({rc}): check the GPU / problem support")
+        self.ctx = h
+        self.batch = 0
+        self._host_inputs = None
+
+    def set_inputs(self, inputs: dict):
+        B = check_contact_inputs(self.prob, inputs)
+        arrs = {k: np.ascontiguousarray(inputs[k], dtype=np.float64) for k in _CONTACT_F64}
+        arrs["cmask"] = np.ascontiguousarray(inputs["cmask"], dtype=np.int32)
+        self._host_inputs = arrs
+        s = ContactInputs(batch=B, memory=MEM_HOST, **{k: _ptr(v) for k, v in arrs.items()})
+        self._check(self.lib.wbq_set_contact_inputs(self.ctx, ctypes.byref(s)), "wbq_set_contact_inputs")
+        self.batch = B
+
+    def set_device_inputs(self, ptrs: dict, batch: int):
+        s = ContactInputs(batch=int(batch), memory=MEM_DEVICE, **{k: int(ptrs[k]) for k in CONTACT_INPUT_FIELDS})
+        self._check(self.lib.wbq_set_contact_inputs(self.ctx, ctypes.byref(s)), "wbq_set_contact_inputs")
+        self.batch = int(batch)
+
+    def x(self):
+        out = np.empty((self.batch, self.prob.nx))
+        self._check(self.lib.wbq_get_contact_outputs(self.ctx, _ptr(out)), "wbq_get_contact_outputs")
+        return out
 
 
 def version() -> str:

@@ -1,0 +1,126 @@
+"""GPU parity of the contact form (ForceAcc): the HIP kernel
+(libwbq, wbq_create_contact) through the C ABI against the CPU oracle
+(oracle/wbq_oracle_contact.c) and the KKT-certified golden fixtures.
+Tolerance (BASELINE north_star): tau within 1e-6 relative per instance,
+rel = ||tau_gpu - tau_ref||_inf / max(1, ||tau_ref||_inf); statuses equal.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden_contact, rel_err
+from qppvm_amd.problem import ContactProblem
+from qppvm_amd.synth import contact_instances, replicate
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+MASKS4 = [0b0011, 0b0111, 0b1111, 0b0101, 0b1010, 0b1100]
+
+
+@pytest.fixture(scope="module")
+def wbq_mod():
+    from qppvm_amd import build, wbq
+    build.build()
+    return wbq
+
+
+def gpu_solve(wbq_mod, prob, inp):
+    s = wbq_mod.ContactSolver(prob, max_batch=max(1, inp["h"].shape[0]))
+    try:
+        tau, st, it = s.solve_batch(inp)
+        return tau, s.x(), st, it
+    finally:
+        s.close()
+
+
+def check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=None):
+    tau_r, x_r, st_r, _, rep = oracle_lib.contact_batch(prob, inp)
+    tau, x, st, it = gpu_solve(wbq_mod, prob, inp)
+    # level-0 repair (y0* != b_w) is not on the GPU yet: those come back as status 2
+    exp_st = np.where(rep != 0, 2, st_r)
+    np.testing.assert_array_equal(st, exp_st)
+    ok = exp_st == 0
+    if min_ok is not None:
+        assert ok.sum() >= min_ok, ok.sum()
+    assert rel_err(tau[ok], tau_r[ok]) <= TOL, rel_err(tau[ok], tau_r[ok])
+    assert rel_err(x[ok], x_r[ok]) <= 1e-5, rel_err(x[ok], x_r[ok])
+    np.testing.assert_array_equal(tau[~ok], inp["h"][~ok])
+    return tau, x, st, it
+
+
+@pytest.mark.parametrize("n", [30, 39])
+def test_contact_golden(wbq_mod, n):
+    for g, prob, inp, exp in load_golden_contact(n):
+        tau, x, st, _ = gpu_solve(wbq_mod, prob, inp)
+        assert np.all(st == 0), (g, st)
+        assert rel_err(tau, exp["tau"]) <= TOL, (g, rel_err(tau, exp["tau"]))
+        assert rel_err(x, exp["x"]) <= 1e-5, (g, rel_err(x, exp["x"]))
+
+
+def test_contact_config1_double_support(wbq_mod, oracle_lib):
+    """BASELINE config 1 contact variant: n = 30, 2 contacts, identical instances."""
+    prob = ContactProblem(n=30, nc=2)
+    inp = replicate(contact_instances(prob, 1, seed=0), 64)
+    tau, x, st, _ = check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=64)
+    assert np.abs(tau - tau[:1]).max() == 0.0  # identical instances, identical answers
+
+
+@pytest.mark.parametrize("nc,masks", [(2, None), (3, [0b011, 0b101, 0b111]), (4, MASKS4), (1, None)])
+def test_contact_random(wbq_mod, oracle_lib, nc, masks):
+    prob = ContactProblem(n=30, nc=nc)
+    inp = contact_instances(prob, 96, seed=40 + nc, masks=masks)
+    check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=96)
+
+
+@pytest.mark.parametrize("n,q", [(30, 0.85), (30, 0.7), (39, 0.8), (20, 0.8)])
+def test_contact_torque_rows(wbq_mod, oracle_lib, n, q):
+    """a12: actuated torque-limit rows, limits at a quantile of the free |tau| (rows bind)."""
+    free = ContactProblem(n=n, nc=4)
+    inp = contact_instances(free, 64, seed=70 + n, masks=MASKS4)
+    tau_free = oracle_lib.contact_batch(free, inp)[0]
+    prob = ContactProblem(n=n, nc=4, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), q)))
+    tau, x, st, _ = check_against_oracle(wbq_mod, oracle_lib, prob, inp)
+    ok = st == 0
+    assert ok.sum() >= 40
+    lim = prob.tau_max[6:] + 1e-7 * np.maximum(1, np.abs(prob.tau_max[6:]))
+    assert np.all(np.abs(tau[ok][:, 6:]) <= lim)
+
+
+def test_contact_structure_and_edges(wbq_mod):
+    """Floating-base torques vanish; inactive feet carry no force; active feet push
+    (f_z >= 10); empty batch; eps_f variants."""
+    prob = ContactProblem(n=30, nc=4)
+    inp = contact_instances(prob, 32, seed=5, masks=MASKS4)
+    tau, x, st, _ = gpu_solve(wbq_mod, prob, inp)
+    assert np.all(st == 0)
+    for b in range(32):
+        f = x[b, 30:].reshape(4, 3)
+        for c in range(4):
+            if (int(inp["cmask"][b]) >> c) & 1:
+                assert f[c, 2] >= 10.0 - 1e-9
+            else:
+                assert np.abs(f[c]).max() == 0.0
+        assert np.abs(tau[b, :6]).max() <= 1e-7 * max(1, np.abs(tau[b]).max())
+    empty = {k: v[:0] for k, v in inp.items()}
+    tau0, x0, st0, _ = gpu_solve(wbq_mod, prob, empty)
+    assert tau0.shape == (0, 30) and st0.shape == (0,)
+
+
+@pytest.mark.parametrize("eps_f", [1e-8, 1e-6, 1e-3])
+def test_contact_eps(wbq_mod, oracle_lib, eps_f):
+    prob = ContactProblem(n=30, nc=4, eps_f=eps_f)
+    inp = contact_instances(prob, 32, seed=9, masks=MASKS4)
+    check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=32)
+
+
+def test_contact_full_batch_properties(wbq_mod):
+    """4096 random instances (BASELINE config 2 size): dynamic feasibility and the force box
+    hold on every instance the GPU solves, all solve."""
+    prob = ContactProblem(n=30, nc=4)
+    inp = contact_instances(prob, 4096, seed=1, masks=[0b0011, 0b0111, 0b1111])
+    tau, x, st, it = gpu_solve(wbq_mod, prob, inp)
+    assert np.all(st == 0)
+    assert np.abs(tau[:, :6]).max() <= 1e-6 * max(1.0, np.abs(tau).max())
+    f = x[:, 30:].reshape(-1, 4, 3)
+    act = ((inp["cmask"][:, None] >> np.arange(4)[None]) & 1).astype(bool)
+    assert np.all(f[act][:, 2] >= 10.0 - 1e-8)
+    assert np.all(np.abs(f[~act]) == 0.0)
