@@ -1,14 +1,32 @@
-"""Throughput bench: batched WBC-QP solves/sec (BASELINE.json metric), QPPVM form, n = 30.
+"""Throughput bench: batched WBC-QP solves/sec (BASELINE.json metric), n = 30.
 
 A step = one wbq_solve over the rank's batch (assemble -> 2-level QP -> tau), inputs
-already resident in HBM. N > 1: one process per GPU (torch.distributed.run), each rank
-solves its own shard of B instances (weak scaling, no data-path collective unless
---allgather). Prints ONE JSON line on rank 0.
+already resident in HBM. Default workload = BASELINE config 1 (4096 identical QPPVM
+instances per GPU); ``--form contact`` runs the contact-form (ForceAcc) variant, and the
+default run also measures that variant for a few hundred steps and reports it beside
+the headline line. ``--config 2`` = random states (QPPVM: ~20 % of torque bounds active;
+contact: 2/3/4 of 4 feet in contact + actuated torque rows).
+
+N > 1: one process per GPU (torch.distributed.run), each rank solves its own shard of B
+instances (weak scaling, no data-path collective unless --allgather). Prints ONE JSON line
+on rank 0.
+
+roofline: achieved = algorithmic bytes of one launch / the dominant kernel's average
+device time (HIP events on the launch stream around that kernel only, on every 8th solve of
+the timed region: event packets on every solve would pace the stream); traffic = HBM
+bytes per launch of that kernel from rocprofv3 PMC passes (FETCH_SIZE x 2, the gfx950
+correction of MI355X_MICROARCH.md, + WRITE_SIZE), run as child processes before this
+process touches the GPU (N = 1 only; --no-pmc skips them).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -16,66 +34,68 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# algorithmic bytes per instance (n = 30, 2 tasks): inputs read once + outputs written once
-def algorithmic_bytes(n, T):
+METRIC = "batched WBC-QP solves/sec, ~30-DoF problem, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+DOMINANT = {"qppvm": "qppvm_fast_kernel", "contact": "contact_kernel"}
+TIMING_EVERY = 8  # HIP-event pairs around every 8th solve of the timed region
+
+
+def qppvm_bytes(n, T):
+    """Algorithmic bytes per QPPVM instance: inputs read once + outputs written once."""
     inputs = 8 * (n * n + T * 6 * n + 2 * T * 12 + 4 * n)  # M, J, pose, pose_ref, q, qd, qref, h
     outputs = 8 * n + 4 + 4  # tau, status, iters
     return inputs + outputs
 
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+def contact_bytes(n, nc):
+    """Algorithmic bytes per contact-form instance."""
+    inputs = 8 * (n * n + 4 * n + 6 * n + 6 + 24 + nc * (6 * n + 6 + 24)) + 4  # ... + cmask
+    outputs = 8 * (n + n + 3 * nc) + 4 + 4  # tau, x, status, iters
+    return inputs + outputs
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
-    ap.add_argument("--n", type=int, default=30)
-    ap.add_argument("--config", type=int, default=1, choices=(1, 2),
-                    help="1: identical instances, bounds inactive; 2: random, ~20%% active bounds")
-    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
-    ap.add_argument("--no-cpu", action="store_true")
-    args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    import torch
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from qppvm_amd.problem import QPPVMProblem
+def build_workload(form, config, n, B, world, rank, device):
+    """(problem, inputs, solver class) for this rank's shard."""
+    from qppvm_amd.problem import ContactProblem, QPPVMProblem
     from qppvm_amd.shard import ShardPlan
-    from qppvm_amd.synth import qppvm_instances, replicate
-    from qppvm_amd.wbq import QPPVMSolver
-
-    n, B = args.n, args.batch
-    device = local if dist else 0
-    if args.config == 1:
-        prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive
-        inp = replicate(qppvm_instances(prob, 1, seed=0), B)
-    else:
-        plan = ShardPlan(B * world, world)  # weak scaling: rank r solves rows [r B, (r+1) B)
+    from qppvm_amd.synth import contact_instances, qppvm_instances, replicate
+    from qppvm_amd.wbq import ContactSolver, QPPVMSolver
+    plan = ShardPlan(B * world, world)  # weak scaling: rank r solves rows [r B, (r+1) B)
+    if form == "qppvm":
+        if config == 1:
+            prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive (SURVEY 8d config 1)
+            return prob, replicate(qppvm_instances(prob, 1, seed=0), B), QPPVMSolver
         inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank))
         # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the first
-        # B instances solved with the limits far away (same sample on every rank, so all ranks
-        # solve one global problem)
+        # B instances solved with the limits far away (same sample on every rank)
         calib = inp if rank == 0 else qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=0)
         free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B, device=device)
         tau_free, _, _ = free.solve_batch(calib)
         free.close()
-        prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
-    solver = QPPVMSolver(prob, max_batch=B, device=device)
+        return QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8))), inp, QPPVMSolver
+    if config == 1:  # double support, identical instances
+        prob = ContactProblem(n=n, nc=2)
+        return prob, replicate(contact_instances(prob, 1, seed=0), B), ContactSolver
+    free = ContactProblem(n=n, nc=4)
+    masks = [0b0011, 0b0111, 0b1111]  # 2, 3 or 4 feet in contact (SURVEY 8d config 2)
+    inp = contact_instances(free, plan.count(rank), seed=1, offset=plan.start(rank), masks=masks)
+    calib = inp if rank == 0 else contact_instances(free, B, seed=1, offset=0, masks=masks)
+    s = ContactSolver(free, max_batch=B, device=device)
+    tau_free, _, _ = s.solve_batch(calib)
+    s.close()
+    prob = ContactProblem(n=n, nc=4, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), 0.85)))
+    return prob, inp, ContactSolver
+
+
+def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False):
+    """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
+    import torch
+    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device)
+    solver = Solver(prob, max_batch=B, device=device)
     solver.set_inputs(inp)
     solver.sync()
-
     gather_buf = None
-    if args.allgather:
+    if allgather:
         # tau goes straight into a torch tensor on torch's stream, then one RCCL all-gather
         out = torch.empty((B, n), dtype=torch.float64, device="cuda")
         gather_buf = torch.empty((world * B, n), dtype=torch.float64, device="cuda")
@@ -86,88 +106,180 @@ def main():
         solver.solve()
         if gather_buf is not None:
             if dist:
+                import torch.distributed as tdist
                 tdist.all_gather_into_tensor(gather_buf, out)
             else:
                 gather_buf.copy_(out)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     solver.sync()
     torch.cuda.synchronize()
     if dist:
+        import torch.distributed as tdist
         tdist.barrier()
-    solver.set_timing(True)
+    solver.set_timing(True, every=TIMING_EVERY)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
+    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (launch-bound if ~ dt)
     solver.sync()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     dt = time.perf_counter() - t0
-    kern_ms, launches = solver.get_timing()
+    solve_ms, kern_ms, launches = solver.get_timing_detail()
     tau, status, iters = solver.outputs()
+    solver.close()
+    kavg_ms, savg_ms = kern_ms / max(launches, 1), solve_ms / max(launches, 1)
     if dist:
-        t = torch.tensor([dt, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt, kavg_ms, savg_ms], dtype=torch.float64, device="cuda")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt, kavg_ms = float(t[0]), float(t[1])
-    else:
-        kavg_ms = kern_ms / max(launches, 1)
-
-    total = B * world * args.steps
-    value = total / dt
-    bytes_per_launch = algorithmic_bytes(n, prob.ntasks) * B
-    achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
-    line = {
-        "metric": "batched WBC-QP solves/sec, ~30-DoF problem, 1/2/4/8 MI355X",
-        "value": value,
-        "unit": "QP-solves/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic randomized robot states (SURVEY 8d), inputs resident in HBM",
-        "config": {"workload": f"QPPVM 2-level torque QP, n={n}, batch={B}/GPU, "
-                               + ("identical instances, bounds inactive (BASELINE config 1)"
-                                  if args.config == 1 else "random states, ~20% bounds active (config 2)"),
-                   "global_batch": B * world, "n": n, "parallelism": f"shard{world}",
-                   "allgather": bool(args.allgather)},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_avg_us": kavg_ms * 1e3,
-                     "algorithmic_bytes_per_instance": algorithmic_bytes(n, prob.ntasks)},
-        "status_ok_frac": float(np.mean(status == 0)),
-        "mean_active_set_steps": float(np.mean(iters)),
-    }
-    if rank == 0 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(prob, inp, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if dist:
-        tdist.destroy_process_group()
+        dt, kavg_ms, savg_ms = float(t[0]), float(t[1]), float(t[2])
+    per_inst = qppvm_bytes(n, prob.ntasks) if form == "qppvm" else contact_bytes(n, prob.nc)
+    return dict(prob=prob, inp=inp, dt=dt, t_enq=t_enq, kavg_ms=kavg_ms, savg_ms=savg_ms, status=status, iters=iters,
+                bytes_per_instance=per_inst, total=B * world * steps)
 
 
-def cpu_baseline(prob, inp, budget_s):
+def pmc_traffic(args, form):
+    """Per-launch HBM bytes of the dominant kernel from two rocprofv3 PMC passes (one counter
+    block each, kernel trace only), child processes of this not-yet-GPU-initialised process."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(td, ctr)
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "run", "--",
+                   sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-pmc", "--no-variant",
+                   "--steps", "20", "--warmup", "2", "--form", form, "--config", str(args.config),
+                   "--batch", str(args.batch), "--n", str(args.n)]
+            env = dict(os.environ, TMPDIR="/tmp")
+            try:
+                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
+            except subprocess.TimeoutExpired:
+                return None, f"{ctr} pass timed out"
+            if r.returncode != 0:
+                return None, f"{ctr} pass failed ({r.returncode})"
+            per = []
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if DOMINANT[form] in row.get("Kernel_Name", ""):
+                            per.append(float(row["Counter_Value"]))
+            if not per:
+                return None, f"{ctr}: no dispatches of {DOMINANT[form]}"
+            vals[ctr] = sum(per) / len(per)  # KB per dispatch
+    fetch, write = vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
+    return {"bytes": 2 * fetch + write, "fetch_raw": fetch, "write": write}, None
+
+
+def cpu_baseline(form, prob, inp, budget_s):
     """The CPU oracle (single thread) on a bounded sample of the same workload."""
     import oracle
     oracle.build()
+    fn = oracle.qppvm_batch if form == "qppvm" else oracle.contact_batch
     done, t0 = 0, time.perf_counter()
     chunk = 64
     B = inp["h"].shape[0]
     while time.perf_counter() - t0 < budget_s:
         lo = done % B
         sl = {k: v[lo:lo + chunk] for k, v in inp.items()}
-        oracle.qppvm_batch(prob, sl)
+        fn(prob, sl)
         done += sl["h"].shape[0]
     dt = time.perf_counter() - t0
+    what = ("x-space OpenSoT-form assembly + BVLS + primal active set" if form == "qppvm" else
+            "contact-form assembly + dense dual active set with LU-solved KKT")
     return {"value": done / dt, "unit": "QP-solves/s", "cores": 1, "kind": "port",
-            "sample": f"{done} instances of the bench batch in {dt:.1f} s, oracle/wbq_oracle.c "
-                      "(x-space OpenSoT-form assembly + BVLS + primal active set), 1 thread"}
+            "sample": f"{done} instances of the bench batch in {dt:.1f} s, oracle ({what}), 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--n", type=int, default=30)
+    ap.add_argument("--form", choices=("qppvm", "contact"), default="qppvm")
+    ap.add_argument("--config", type=int, default=1, choices=(1, 2),
+                    help="1: identical instances; 2: random states, bounds / contacts churn")
+    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--no-variant", action="store_true", help="skip the contact-form variant line")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    traffic, traffic_note = None, "skipped (--no-pmc or N > 1)"
+    if not dist and not args.no_pmc:
+        traffic, traffic_note = pmc_traffic(args, args.form)  # before this process touches the GPU
+    import torch
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = local if dist else 0
+    n, B = args.n, args.batch
+    m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, args.allgather, dist)
+    value = m["total"] / m["dt"]
+    bpl = m["bytes_per_instance"] * B
+    achieved = bpl / (m["kavg_ms"] * 1e-3) / 1e9
+    wl = {("qppvm", 1): "QPPVM 2-level torque QP, identical instances, bounds inactive (BASELINE config 1)",
+          ("qppvm", 2): "QPPVM 2-level torque QP, random states, ~20% torque bounds active (config 2)",
+          ("contact", 1): "ForceAcc contact-form QP, double support (nc=2), identical instances (config 1 variant)",
+          ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows (config 2)"}
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "QP-solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": m["dt"] * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic randomized robot states (SURVEY 8d), inputs resident in HBM",
+        "config": {"workload": f"{wl[(args.form, args.config)]}, n={n}, batch={B}/GPU",
+                   "global_batch": B * world, "n": n, "parallelism": f"shard{world}",
+                   "allgather": bool(args.allgather)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None if traffic is None else traffic["bytes"],
+                     "kernel": DOMINANT[args.form], "kernel_avg_us": m["kavg_ms"] * 1e3,
+                     "solve_avg_us": m["savg_ms"] * 1e3, "algorithmic_bytes_per_launch": bpl,
+                     "algorithmic_bytes_per_instance": m["bytes_per_instance"],
+                     "traffic_note": traffic_note if traffic is None else
+                     "rocprofv3 PMC per launch: 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE"
+                     f"; raw fetch {traffic['fetch_raw']:.0f} B, write {traffic['write']:.0f} B"},
+        "status_ok_frac": float(np.mean(m["status"] == 0)),
+        "mean_active_set_steps": float(np.mean(m["iters"])),
+        "host_enqueue_us_per_step": m["t_enq"] * 1e6 / args.steps,
+    }
+    if not args.no_variant and args.form == "qppvm":
+        # the contact-form variant of the same config, same process, same protocol
+        v = run("contact", args.config, n, B, max(50, args.steps // 2), args.warmup, world, rank, device,
+                False, dist)
+        va = v["bytes_per_instance"] * B / (v["kavg_ms"] * 1e-3) / 1e9
+        line["contact_variant"] = {"workload": wl[("contact", args.config)], "value": v["total"] / v["dt"],
+                                   "ms_per_step": v["dt"] * 1e3 / max(50, args.steps // 2),
+                                   "kernel_avg_us": v["kavg_ms"] * 1e3, "roofline_frac": va / HBM_PEAK_GBS,
+                                   "status_ok_frac": float(np.mean(v["status"] == 0)),
+                                   "mean_active_set_steps": float(np.mean(v["iters"]))}
+    if rank == 0 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.form, m["prob"], m["inp"], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -155,10 +155,13 @@ int wbq_get_device_outputs(wbq_ctx *ctx, const double **tau, const int32_t **sta
                            const int32_t **iters);
 /* Drop the warm-start working set of instances with mask[b] != 0 (NULL = all). */
 int wbq_reset_warmstart(wbq_ctx *ctx, const uint8_t *mask);
-/* Kernel timing with HIP events on the launch stream: enable, then read the summed
- * device time (ms) and the number of timed launches since the last read. */
+/* Kernel timing with HIP events on the launch stream: enable = N > 0 times every N-th solve
+ * (events are stream packets: sampling keeps them from pacing the stream), 0 disables; then
+ * read the summed device time (ms) and the number of timed solves since the last read. */
 int wbq_set_timing(wbq_ctx *ctx, int enable);
 int wbq_get_timing(wbq_ctx *ctx, double *total_ms, int *launches);
+/* Same, split: summed device time of whole solves and of their dominant (first) kernel. */
+int wbq_get_timing_detail(wbq_ctx *ctx, double *solve_ms, double *kernel_ms, int *launches);
 void wbq_destroy(wbq_ctx *ctx);
 const char *wbq_last_error(const wbq_ctx *ctx);
 const char *wbq_version(void);

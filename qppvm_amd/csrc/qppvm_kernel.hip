@@ -763,9 +763,19 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     return Mr.dot(S + L.U, NP);
 }
 
-// Active-set kernel: same instance -> block mapping as the fast kernel; blocks without a
-// parked instance (status -1) exit at once. An instance whose active set finds level 0
-// infeasible is handed on to the repair kernel with status -2.
+// Work lists: the producing kernel appends every instance that needs a follow-up kernel
+// (atomic counter work[epoch*2 + 0] / [+1], lists wl[0..B) / wl[B..2B)), and the follow-up
+// kernels run a small grid-stride grid over the list. Without work a launch is one
+// broadcast load per block of at most kFollowGrid blocks, instead of a batch-sized grid.
+__device__ __forceinline__ void wl_push(const QppvmArgs &a, int list, long b)
+{
+    const int idx = atomicAdd(&a.work[a.epoch * 2 + list], 1);
+    a.wl[(long)list * a.B + idx] = (int)b;
+}
+
+// Active-set kernel (NP = 64; NP = 32 runs it inline in the fast kernel): instances parked
+// with status -1. An instance whose active set finds level 0 infeasible is handed on to the
+// repair kernel with status -2.
 template <int NP, int M0>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
 {
@@ -776,42 +786,44 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
-    if (a.work[a.epoch * 2] == 0) return; // nothing parked in this solve
-    const long b0_ = (long)blockIdx.x * IPW + sub;
-    const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -1;
-    if (!__any(valid)) return;
-    WBQ_STAMP(4);
-    const long b = valid ? b0_ : 0;
-    const int n = a.n;
-    const bool row = valid && i < n;
-    const double h_i = row ? a.h[b * n + i] : 0.0;
-    const double lo = row ? a.tau_min[i] - h_i : -kInf;
-    const double hi = row ? a.tau_max[i] - h_i : kInf;
-    const double *qs = a.q1_scr + b * kM0Max * NP;
+    const int cnt = a.work[a.epoch * 2]; // instances parked in this solve
+    for (long e0 = (long)blockIdx.x * IPW; e0 < cnt; e0 += (long)gridDim.x * IPW) {
+        const long e = e0 + sub;
+        const bool valid = e < cnt;
+        WBQ_STAMP(4);
+        const long b = valid ? a.wl[e] : 0;
+        const int n = a.n;
+        const bool row = valid && i < n;
+        const double h_i = row ? a.h[b * n + i] : 0.0;
+        const double lo = row ? a.tau_min[i] - h_i : -kInf;
+        const double hi = row ? a.tau_max[i] - h_i : kInf;
+        const double *qs = a.q1_scr + b * kM0Max * NP;
+        __syncthreads(); // the previous instance's LDS is dead
 #pragma unroll
-    for (int c = 0; c < NP; ++c)
-        S[L.QA + c * RS + i] = (valid && c < M0 && c < a.m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
-    int status = 0, iters = 0;
-    bool infeasible = false;
-    WBQ_STAMP(6);
-    const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0, status,
-                                        iters, infeasible);
-    if (infeasible) {
-        if (valid && i == 0) {
-            a.status[b] = -2; // level-0 repair kernel
-            a.work[a.epoch * 2 + 1] = 1;
+        for (int c = 0; c < NP; ++c)
+            S[L.QA + c * RS + i] = (valid && c < M0 && c < a.m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
+        int status = 0, iters = 0;
+        bool infeasible = false;
+        WBQ_STAMP(6);
+        const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0,
+                                            status, iters, infeasible);
+        if (infeasible) {
+            if (valid && i == 0) {
+                a.status[b] = -2; // level-0 repair kernel
+                wl_push(a, 1, b);
+            }
+        } else {
+            double tau_i = x_i + h_i;
+            if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+            if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+            if (row) a.tau[b * n + i] = tau_i;
+            if (valid && i == 0) {
+                a.status[b] = status;
+                a.iters[b] = iters;
+            }
         }
-    } else {
-        double tau_i = x_i + h_i;
-        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
-        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
-        if (row) a.tau[b * n + i] = tau_i;
-        if (valid && i == 0) {
-            a.status[b] = status;
-            a.iters[b] = iters;
-        }
+        WBQ_STAMP(7);
     }
-    WBQ_STAMP(7);
 }
 
 // Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by the
@@ -826,37 +838,40 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's flags (its parity was last used
-        a.work[(a.epoch ^ 1) * 2] = 0;         // by the previous solve, which has completed)
+    const int cnt = a.work[a.epoch * 2 + 1]; // instances flagged for the level-0 repair
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's counters (its parity was last
+        a.work[(a.epoch ^ 1) * 2] = 0;         // used by the previous solve, which has completed)
         a.work[(a.epoch ^ 1) * 2 + 1] = 0;
     }
-    if (a.work[a.epoch * 2 + 1] == 0) return; // no level-0 repair in this solve
-    const long b0_ = (long)blockIdx.x * IPW + sub;
-    const bool valid = b0_ < a.B && a.status[b0_ < a.B ? b0_ : 0] == -2;
-    if (!__any(valid)) return;
-    const long b = valid ? b0_ : 0;
-    const int n = a.n;
-    const bool row = valid && i < n;
-    const double h_i = row ? a.h[b * n + i] : 0.0;
-    WBQ_STAMP(8);
-    const bool warm = valid && a.ws_hint[b] != 0;
-    const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid, row ? a.tau_min[i] - h_i : -kInf,
-                                               row ? a.tau_max[i] - h_i : kInf, warm);
-    WBQ_STAMP(11);
-    int status = ro.status, iters = 0;
-    bool infeasible = false;
-    const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status, iters,
-                                        infeasible);
-    WBQ_STAMP(12);
-    if (infeasible && status == 0) status = 2;
-    double tau_i = x_i + h_i;
-    if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
-    if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
-    if (row) a.tau[b * n + i] = tau_i;
-    if (valid && i == 0) {
-        a.status[b] = status;
-        a.iters[b] = iters + ro.it;
-        a.ws_hint[b] = ro.l0inf ? 1 : 0;
+    for (long e0 = (long)blockIdx.x * IPW; e0 < cnt; e0 += (long)gridDim.x * IPW) {
+        const long e = e0 + sub;
+        const bool valid = e < cnt;
+        const long b = valid ? a.wl[a.B + e] : 0;
+        const int n = a.n;
+        const bool row = valid && i < n;
+        const double h_i = row ? a.h[b * n + i] : 0.0;
+        WBQ_STAMP(8);
+        __syncthreads(); // the previous instance's LDS is dead
+        const bool warm = valid && a.ws_hint[b] != 0;
+        const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid,
+                                                   row ? a.tau_min[i] - h_i : -kInf, row ? a.tau_max[i] - h_i : kInf,
+                                                   warm);
+        WBQ_STAMP(11);
+        int status = ro.status, iters = 0;
+        bool infeasible = false;
+        const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status,
+                                            iters, infeasible);
+        WBQ_STAMP(12);
+        if (infeasible && status == 0) status = 2;
+        double tau_i = x_i + h_i;
+        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+        if (row) a.tau[b * n + i] = tau_i;
+        if (valid && i == 0) {
+            a.status[b] = status;
+            a.iters[b] = iters + ro.it;
+            a.ws_hint[b] = ro.l0inf ? 1 : 0;
+        }
     }
 }
 
@@ -1132,7 +1147,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
                 if (inf || to_rep) {
                     if (i == 0) {
                         a.status[b] = -2;
-                        a.work[a.epoch * 2 + 1] = 1;
+                        wl_push(a, 1, b);
                     }
                 } else {
                     double tau2 = x2 + h_i;
@@ -1154,7 +1169,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
                 if (c < m0) qs[c * NP + i] = q1[c];
             if (i == 0) {
                 a.status[b] = to_rep ? -2 : -1; // picked up by the active-set / repair kernel
-                a.work[a.epoch * 2 + (to_rep ? 1 : 0)] = 1;
+                wl_push(a, to_rep ? 1 : 0, b);
             }
         }
     }
@@ -1175,8 +1190,10 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
     return hipGetLastError();
 }
 
+constexpr unsigned kFollowGrid = 512; // 2 blocks per CU
+
 template <int NP, int M0>
-hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
+hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     constexpr int IPW = kWave / NP;
     static size_t attr_fast = 0, attr_active = 0, attr_repair = 0;
@@ -1186,17 +1203,25 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream)
     hipError_t e = launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED>, a, grid, stream,
                                                              attr_fast);
     if (e != hipSuccess) return e;
-    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, grid, stream, attr_active);
+    if (mid) { // end of the dominant launch
+        e = hipEventRecord(mid, stream);
+        if (e != hipSuccess) return e;
+    }
+    // follow-up kernels: grid-stride over their work lists, at most kFollowGrid blocks
+    const unsigned fgrid = grid < kFollowGrid ? grid : kFollowGrid;
+    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream, attr_active);
     if (e != hipSuccess) return e;
-    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, grid, stream, attr_repair);
+    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream, attr_repair);
 }
 
 }  // namespace
 
-hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream)
+bool qppvm_single_launch(int) { return false; }
+
+hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
-    if (a.n <= 32) return a.m0 <= 6 ? launch_np<32, 6>(a, stream) : launch_np<32, kM0Max>(a, stream);
-    return a.m0 <= 6 ? launch_np<64, 6>(a, stream) : launch_np<64, kM0Max>(a, stream);
+    if (a.n <= 32) return a.m0 <= 6 ? launch_np<32, 6>(a, stream, mid) : launch_np<32, kM0Max>(a, stream, mid);
+    return a.m0 <= 6 ? launch_np<64, 6>(a, stream, mid) : launch_np<64, kM0Max>(a, stream, mid);
 }
 
 }  // namespace wbq

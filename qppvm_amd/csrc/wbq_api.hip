@@ -50,15 +50,20 @@ struct wbq_ctx {
     int *out_iters = nullptr;
     // event timing
     bool timing = false;
-    std::vector<hipEvent_t> ev;  // pairs
+    int timing_every = 1;       // time every timing_every-th solve
+    unsigned long long solves = 0;
+    std::vector<hipEvent_t> ev;  // triples (start, end of the dominant kernel, end)
+    std::vector<int> ev_mid;     // per triple: index of the event ending the dominant kernel
     int ev_used = 0;
     double t_acc_ms = 0.0;
+    double t_kern_ms = 0.0;
     int t_launches = 0;
     std::string err;
     unsigned long long *stamps = nullptr; // diagnostic builds only
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
     double *ui_scr = nullptr, *b0_scr = nullptr; // u_imp and b0 for the level-0 repair
-    int *work = nullptr; // [2][2] per-solve work flags (see wbq_kernels.h)
+    int *work = nullptr; // [2][2] per-solve work counters (see wbq_kernels.h)
+    int *wl = nullptr;   // [2][max_batch] work lists
     unsigned char *ws_hint = nullptr; // [B] warm start (see wbq_kernels.h)
     signed char *ws_state = nullptr;  // [B][NP]
     size_t np = 0;
@@ -157,12 +162,14 @@ int solve_contact(wbq_ctx *c)
     a.iters = c->out_iters ? c->out_iters : c->iters;
     a.x = c->dev_x;
     WBQ_HIP(hipSetDevice(c->device));
-    const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
+    const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
+                       (c->solves++ % (unsigned long long)c->timing_every) == 0;
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
     WBQ_HIP(wbq::launch_contact(a, c->stream));
-    if (timed) {
-        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-        c->ev_used += 2;
+    if (timed) { // one kernel: the dominant kernel is the whole solve
+        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 2], c->stream));
+        c->ev_mid[c->ev_used / 3] = 2;
+        c->ev_used += 3;
     }
     return WBQ_SUCCESS;
 }
@@ -242,6 +249,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess &&
              hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
+             hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
              hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
              hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
         c->np = np;
@@ -455,18 +463,24 @@ int wbq_solve(wbq_ctx *c)
     a.ui_scr = c->ui_scr;
     a.b0_scr = c->b0_scr;
     a.work = c->work;
+    a.wl = c->wl;
     a.epoch = c->epoch;
     a.ws_hint = c->ws_hint;
     a.ws_state = c->ws_state;
 
     WBQ_HIP(hipSetDevice(c->device));
-    const bool timed = c->timing && c->ev_used + 2 <= (int)c->ev.size();
+    // timed solves record (start, after the dominant first kernel, end) on the launch stream
+    const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
+                       (c->solves++ % (unsigned long long)c->timing_every) == 0;
+    const bool single = wbq::qppvm_single_launch(a.n);
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
-    WBQ_HIP(wbq::launch_qppvm(a, c->stream));
+    WBQ_HIP(wbq::launch_qppvm(a, c->stream, (timed && !single) ? c->ev[c->ev_used + 1] : nullptr));
     if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
     if (timed) {
-        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-        c->ev_used += 2;
+        // one launch: the end event also ends the dominant kernel (no extra event in the stream)
+        WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 2], c->stream));
+        c->ev_mid[c->ev_used / 3] = single ? 2 : 1;
+        c->ev_used += 3;
     }
     return WBQ_SUCCESS;
 }
@@ -547,33 +561,46 @@ int wbq_set_timing(wbq_ctx *c, int enable)
     if (!c) return WBQ_E_INVALID;
     WBQ_HIP(hipSetDevice(c->device));
     if (enable && c->ev.empty()) {
-        c->ev.resize(2 * 4096);
+        c->ev.resize(3 * 4096);
+        c->ev_mid.assign(4096, 2);
         for (auto &e : c->ev) WBQ_HIP(hipEventCreate(&e));
     }
-    c->timing = enable != 0;
+    c->timing = enable > 0;
+    c->timing_every = enable > 0 ? enable : 1;
+    c->solves = 0;
     c->ev_used = 0;
     c->t_acc_ms = 0.0;
+    c->t_kern_ms = 0.0;
+    c->t_launches = 0;
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_timing_detail(wbq_ctx *c, double *solve_ms, double *kernel_ms, int *launches)
+{
+    if (!c) return WBQ_E_INVALID;
+    WBQ_HIP(hipSetDevice(c->device));
+    for (int k = 0; k + 2 < c->ev_used; k += 3) {
+        WBQ_HIP(hipEventSynchronize(c->ev[k + 2]));
+        float ms = 0.f, km = 0.f;
+        WBQ_HIP(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 2]));
+        WBQ_HIP(hipEventElapsedTime(&km, c->ev[k], c->ev[k + c->ev_mid[k / 3]]));
+        c->t_acc_ms += ms;
+        c->t_kern_ms += km;
+        c->t_launches += 1;
+    }
+    c->ev_used = 0;
+    if (solve_ms) *solve_ms = c->t_acc_ms;
+    if (kernel_ms) *kernel_ms = c->t_kern_ms;
+    if (launches) *launches = c->t_launches;
+    c->t_acc_ms = 0.0;
+    c->t_kern_ms = 0.0;
     c->t_launches = 0;
     return WBQ_SUCCESS;
 }
 
 int wbq_get_timing(wbq_ctx *c, double *total_ms, int *launches)
 {
-    if (!c) return WBQ_E_INVALID;
-    WBQ_HIP(hipSetDevice(c->device));
-    for (int k = 0; k + 1 < c->ev_used; k += 2) {
-        WBQ_HIP(hipEventSynchronize(c->ev[k + 1]));
-        float ms = 0.f;
-        WBQ_HIP(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
-        c->t_acc_ms += ms;
-        c->t_launches += 1;
-    }
-    c->ev_used = 0;
-    if (total_ms) *total_ms = c->t_acc_ms;
-    if (launches) *launches = c->t_launches;
-    c->t_acc_ms = 0.0;
-    c->t_launches = 0;
-    return WBQ_SUCCESS;
+    return wbq_get_timing_detail(c, total_ms, nullptr, launches);
 }
 
 #ifdef WBQ_STAMPS
@@ -607,6 +634,7 @@ void wbq_destroy(wbq_ctx *c)
     if (c->ui_scr) (void)hipFree(c->ui_scr);
     if (c->b0_scr) (void)hipFree(c->b0_scr);
     if (c->work) (void)hipFree(c->work);
+    if (c->wl) (void)hipFree(c->wl);
     if (c->ws_hint) (void)hipFree(c->ws_hint);
     if (c->ws_state) (void)hipFree(c->ws_state);
     if (c->dev_x) (void)hipFree(c->dev_x);

@@ -34,11 +34,12 @@ struct QppvmArgs {
     double *q1_scr;  // [B][kM0Max][NP]  Q1 = G^T L^-T
     double *ui_scr;  // [B][NP]   u_imp = M^-1 tau_imp
     double *b0_scr;  // [B][kM0Max]  b0 = G w_t (level-0 targets)
-    // per-solve work flags, double-buffered by solve parity: work[epoch*2 + 0] = some instance
-    // parked for the active-set kernel, [+1] = some for the repair kernel. A follow-up
-    // kernel with no work exits on one broadcast load; the repair kernel (the last launch)
-    // clears the other parity's flags for the next solve.
-    int *work;       // [2][2]
+    // per-solve work lists, double-buffered by solve parity: work[epoch*2 + 0] counts the
+    // instances parked for the active-set kernel (listed in wl[0, B)), [+1] those for the
+    // repair kernel (wl[B, 2B)). The follow-up kernels run small grid-stride grids over the
+    // lists; the repair kernel (the last launch) clears the other parity's counters.
+    int *work;       // [2][2] counters: instances appended to the two work lists this solve
+    int *wl;         // [2][B] work lists: [0, B) active-set kernel, [B, 2B) repair kernel
     int epoch;       // 0 / 1
     // per-instance warm start across solves (the qpOASES hot-start analogue; it changes the
     // path, never the solution): hint = the last solve needed the level-0 repair, so go there
@@ -50,7 +51,10 @@ struct QppvmArgs {
 constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
 
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
-hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream);
+// mid (optional): recorded on the stream right after the first (dominant) kernel when a
+// second launch follows (n > 32); n <= 32 is one launch (qppvm_single_launch).
+bool qppvm_single_launch(int n);
+hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 
 // ------------------------------------------------------------------ contact form (ForceAcc)
 constexpr int kCMax = 4; // contacts

@@ -24,7 +24,7 @@ FORM_QPPVM, FORM_CONTACT = 0, 1
 EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
            "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
-           "wbq_set_contact_inputs", "wbq_get_contact_outputs")
+           "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail")
 
 
 class WbqError(RuntimeError):
@@ -84,6 +84,8 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_reset_warmstart.argtypes = [P, P]
     lib.wbq_set_timing.argtypes = [P, I]
     lib.wbq_get_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I)]
+    lib.wbq_get_timing_detail.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(I)]
     lib.wbq_destroy.argtypes = [P]
     lib.wbq_destroy.restype = None
     lib.wbq_last_error.argtypes = [P]
@@ -95,7 +97,7 @@ def load_library(path: str = LIB_PATH):
     for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
               "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
               "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
-              "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing"):
+              "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib
@@ -206,8 +208,9 @@ class QPPVMSolver:
                     "wbq_reset_warmstart")
 
     # -- timing (HIP events around every launch, on the launch stream)
-    def set_timing(self, enable: bool):
-        self._check(self.lib.wbq_set_timing(self.ctx, int(bool(enable))), "wbq_set_timing")
+    def set_timing(self, enable: bool, every: int = 1):
+        """Time every ``every``-th solve with HIP events (0 / False disables)."""
+        self._check(self.lib.wbq_set_timing(self.ctx, int(every) if enable else 0), "wbq_set_timing")
 
     def get_timing(self):
         ms = ctypes.c_double()
@@ -215,6 +218,14 @@ class QPPVMSolver:
         self._check(self.lib.wbq_get_timing(self.ctx, ctypes.byref(ms), ctypes.byref(cnt)),
                     "wbq_get_timing")
         return ms.value, cnt.value
+
+    def get_timing_detail(self):
+        """(summed solve ms, summed dominant-kernel ms, timed solves) since the last read."""
+        ms, km = ctypes.c_double(), ctypes.c_double()
+        cnt = ctypes.c_int()
+        self._check(self.lib.wbq_get_timing_detail(self.ctx, ctypes.byref(ms), ctypes.byref(km),
+                                                   ctypes.byref(cnt)), "wbq_get_timing_detail")
+        return ms.value, km.value, cnt.value
 
 
 class ContactSolver(QPPVMSolver):

@@ -17,13 +17,14 @@ run() { # name, timeout, cmd...
 run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ; rc=$?
 if [ $rc -ge 2 ]; then echo "pytest crashed/timed out ($rc): stopping"; exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
-run bench 300 python bench.py --steps 200 --warmup 20 || exit 1
+run bench 400 python bench.py --steps 200 --warmup 20 || exit 1
 if [ "$STEPS" = "all" ]; then
-  run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
+  run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu --no-pmc --no-variant || exit 1
+  run bench_contact_cfg2 300 python bench.py --form contact --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
   cd /tmp && run_dir="$GRAFT_REPO_ROOT/gpurun_out/prof"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$run_dir" -o run --output-format csv -- \
-      python "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
-  echo "prof rc=$?"; tail -n 5 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"
+      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu --no-pmc > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  echo "prof rc=$?"; tail -n 2 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"
 fi
 if [ "$STEPS" = "all" ] || [ "$STEPS" = "plugin" ]; then
   cd "$GRAFT_REPO_ROOT"

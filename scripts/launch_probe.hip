@@ -13,6 +13,15 @@ __global__ __launch_bounds__(64, 2) void probe(const int *flag, double *out)
     out[blockIdx.x * 64 + threadIdx.x] = sm[63 - threadIdx.x];
 }
 
+// same, but the (never taken) work path needs ~1 KB of scratch per lane, like the repair kernel
+__global__ __launch_bounds__(64, 2) void probe_scratch(const int *flag, double *out, int k)
+{
+    if (*flag == 0) return;
+    volatile double buf[128];
+    for (int j = 0; j < 128; ++j) buf[j] = j * out[j];
+    out[blockIdx.x * 64 + threadIdx.x] = buf[(threadIdx.x + k) & 127];
+}
+
 __global__ __launch_bounds__(64, 2) void busy(double *out, int iters)
 {
     double v = threadIdx.x;
@@ -77,6 +86,49 @@ int main()
         float ms;
         hipEventElapsedTime(&ms, e0, e1);
         std::printf("busy + %d no-work kernels (grid 256, 20 KB): %.3f us/iter\n", extra, 1e3 * ms / N);
+    }
+    // the same with a scratch-using no-work kernel, and as a hipGraph
+    for (int g : {256, 512, 2048}) {
+        const int N = 500;
+        hipEventRecord(e0, s);
+        for (int k = 0; k < N; ++k) {
+            hipLaunchKernelGGL(busy, dim3(2048), dim3(64), 0, s, out, 20000);
+            hipLaunchKernelGGL(probe_scratch, dim3(g), dim3(64), 20480, s, flag, out, k);
+        }
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        std::printf("busy + 1 scratch no-work kernel (grid %d, 20 KB): %.3f us/iter\n", g, 1e3 * ms / N);
+    }
+    {
+        hipGraph_t gr;
+        hipGraphExec_t ge;
+        hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+        hipLaunchKernelGGL(busy, dim3(2048), dim3(64), 0, s, out, 20000);
+        hipLaunchKernelGGL(probe_scratch, dim3(512), dim3(64), 20480, s, flag, out, 1);
+        hipStreamEndCapture(s, &gr);
+        hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+        for (int w = 0; w < 20; ++w) hipGraphLaunch(ge, s);
+        hipStreamSynchronize(s);
+        const int N = 500;
+        hipEventRecord(e0, s);
+        for (int k = 0; k < N; ++k) hipGraphLaunch(ge, s);
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        std::printf("graph(busy + scratch no-work grid 512): %.3f us/iter\n", 1e3 * ms / N);
+    }
+    {
+        const int N = 500;
+        hipEventRecord(e0, s);
+        for (int k = 0; k < N; ++k) hipLaunchKernelGGL(busy, dim3(2048), dim3(64), 0, s, out, 20000);
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        std::printf("busy alone: %.3f us/iter\n", 1e3 * ms / N);
     }
     return 0;
 }
