@@ -27,8 +27,9 @@
 // taken exactly in x-space, restore full fp64 accuracy (scripts/emulate_contact.py: 1e-5
 // relative without, 1e-12 with). A final re-check of every row guards the active set itself.
 //
-// Joint rows double as the torque output: tau_i = (row i of [M | -J_lin^T]) x + h_i, the
-// activity of joint row i, whether or not it is a constraint.
+// Torque output: tau_i = (row i of [M | -J_lin^T]) x + h_i from lane i's own M row and
+// contact-Jacobian column, held in registers since the stage; only the joint rows that are
+// constraints (the 6 floating-base rows, or all with torque rows) are kept in LDS.
 //
 // Statuses: 0 ok, 1 step cap, 2 infeasible (level 0 not attainable at b_w, or no feasible
 // point), 3 numerical. On status != 0: tau = h, x = 0.
@@ -46,7 +47,7 @@ namespace {
 // X = H^-1 A_q^T has one column ("slot") per q-bearing row, slot = ci, plus x0 at NJ + 6.
 struct ContactLayout {
     int NJ, NR, ME, NX, QS, FS, GS, TS;
-    int AQJ, AQW, FFJ, XT, GM, TT, JC, PN, RH, HR, XV, X0, VV, LV, RV, AC, PS, BT, JD, QD, SIZE;
+    int AQJ, AQW, FFJ, XT, GM, TT, TC, GA, JC, PN, RH, HR, XV, X0, VV, LV, RV, WV, DUM, AC, PS, BT, JD, QD, SIZE;
     __host__ __device__ ContactLayout(int n, int nc, bool tr, int NQ, int NRC)
     {
         NJ = tr ? n : 6;
@@ -56,26 +57,31 @@ struct ContactLayout {
         QS = NQ + 1;          // row stride of NQ-wide rows (odd: lane-per-row reads conflict-free)
         FS = 3 * nc + 1;
         GS = ME | 1;
-        TS = NX | 1;          // the active set never exceeds NX independent rows
+        TS = (NX + 8) | 1;    // the active set never exceeds NX independent rows (+8: chunked dots)
         int o = 0;
-        AQJ = o; o += n * QS;     // joint rows, acceleration part: M row a
+        AQJ = o; o += NJ * QS;    // joint constraint rows, acceleration part: M row a
         AQW = o; o += 6 * QS;     // waist rows: J_w row r
-        FFJ = o; o += n * FS;     // joint rows, force part: -J_c[0:3, a] (active contacts)
+        FFJ = o; o += NJ * FS;    // their force part: -J_c[0:3, a] (active contacts)
         XT = o; o += NR * QS;     // X^T: slot s = column s of H^-1 A_q^T over the qdd lanes
         GM = o; o += ME * GS;     // Gamma
         TT = o;                   // T = L^-1 of the active-set Gram, rows of TS
         int ov = 0;               // setup-phase overlays of the TT region
-        JC = TT + ov; ov += 6 * kCMax * NQ;   // contact Jacobian rows
-        PN = TT + ov; ov += 2 * 64 * 4;       // Gauss-Jordan pivot panel
+        JC = TT + ov; ov += 6 * nc * NQ;      // contact Jacobian rows
+        PN = TT + ov; ov += 2 * NQ * 4;       // Gauss-Jordan pivot panel (rows < NQ publish)
         RH = TT + ov; ov += 2 * 4 * NRC;      // its right-hand sides
         HR = TT + ov; ov += (NQ == 64 && tr) ? NQ * QS : 0; // H rows for a second rhs chunk
-        const int tt = NX * TS;
+        // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns
+        const int tt = tr ? (2 * NX + ME) * TS : 12 * TS; // (!tr: scratch for the T_E rows)
+        TC = TT + NX * TS;
+        GA = TC + NX * TS;
         o += tt > ov ? tt : ov;
         XV = o; o += 64;          // x
         X0 = o; o += 64;          // x0 = -H^-1 g
-        VV = o; o += 64;
-        LV = o; o += 64;
-        RV = o; o += 64;
+        VV = o; o += 72;          // (slot dots read 8 past the active count)
+        LV = o; o += 72;
+        RV = o; o += 72;
+        WV = o; o += 72;
+        DUM = o; o += 72;         // row of the lanes that own no slot-vector row
         AC = o; o += 64;          // active constraint (compact index) per slot
         PS = o; o += 24 * (1 + kCMax);   // poses: waist, then contacts ([R|p], ref)
         BT = o; o += 6 * (1 + kCMax);    // task targets: waist b_w, then b_c
@@ -101,97 +107,153 @@ __device__ __forceinline__ double fcoef(const double *S, const ContactLayout &L,
     return (ci - L.NJ - 6 == f) ? 1.0 : 0.0;
 }
 
-// activity a_ci . x of constraint row ci at x = XV (n qdd entries, then nf forces)
+// activity a_ci . x of constraint row ci at x = XV (n qdd entries, then nf forces); loads
+// in chunks of 8 so they issue back to back
+template <int NQ>
 __device__ __forceinline__ double activity(const double *S, const ContactLayout &L, int ci, int n, int nf)
 {
     const double *xv = S + L.XV;
+    const bool jrow = ci < L.NJ, wrow = !jrow && ci < L.NJ + 6;
+    const double *rq = S + (jrow ? L.AQJ + ci * L.QS : (wrow ? L.AQW + (ci - L.NJ) * L.QS : L.AQW));
     double s = 0.0;
-    const double *rq = row_q(S, L, ci);
-    if (rq) {
-        for (int j = 0; j < n; ++j) s = fma(rq[j], xv[j], s);
-    }
-    if (ci < L.NJ) {
-        for (int f = 0; f < nf; ++f) s = fma(S[L.FFJ + ci * L.FS + f], xv[n + f], s);
-    } else if (ci >= L.NJ + 6) {
-        s = xv[n + ci - L.NJ - 6];
-    }
-    return s;
-}
-
-// Append slot a (compact row c, sign sg) to T = L^-1 of the active-set Gram: with
-// v_c' = sg_c' sg Gamma[act_c'][c] (c' < a), l = T v, d^2 = Gamma_cc - l.l, the new row is
-// [-(T^T l)^T / d, 1/d]. Returns d^2 (<= 0: dependent). Lane i < a owns slot i.
-__device__ __forceinline__ double t_append(double *S, const ContactLayout &L, int i, int a, int c, double sg,
-                                           int act, double sgn)
-{
-    if (i < a) S[L.VV + i] = sgn * sg * S[L.GM + act * L.GS + c];
-    __syncthreads();
-    double l = 0.0;
-    if (i < a)
-        for (int q = 0; q <= i; ++q) l = fma(S[L.TT + i * L.TS + q], S[L.VV + q], l);
-    S[L.LV + i] = l;
-    __syncthreads();
-    double r = 0.0;
-    if (i < a)
-        for (int q = i; q < a; ++q) r = fma(S[L.TT + q * L.TS + i], S[L.LV + q], r);
-    const double d2 = S[L.GM + c * L.GS + c] - isum<64>(l * l);
-    const double id = d2 > 0.0 ? frsq(d2) : 0.0;
-    if (i < a) S[L.TT + a * L.TS + i] = -r * id;
-    if (i == a) S[L.TT + a * L.TS + a] = id;
-    __syncthreads();
-    return d2;
-}
-
-// x = x0 + H^-1 A_A^T (sgn lam), then two steps of iterative refinement of (x, lambda) on the
-// active set: residual of the active rows in x-space (exact to roundoff), correction through
-// the same T. Lane i < k owns slot i; lane v < NX owns x_v. Leaves x in XV.
-__device__ __noinline__ void rebuild_refine(double *S, const ContactLayout &L, int i, int k, int n, int nf, int act,
-                                            double sgn, double &lam, double lo, double hi, double ieps)
-{
-    const int NJ = L.NJ;
-    // shuffles with every lane active (the source lane of a slot is any constraint lane)
-    const double lo_a = __shfl(lo, act), hi_a = __shfl(hi, act);
-    S[L.RV + i] = i < k ? sgn * lam : 0.0;
-    S[L.AC + i] = (double)act;
-    __syncthreads();
-    for (int pass = 0; pass < 3; ++pass) {
-        if (pass > 0) {
-            __syncthreads();
-            double res = 0.0;
-            if (i < k) res = sgn * ((sgn > 0.0 ? lo_a : hi_a) - activity(S, L, act, n, nf));
-            S[L.VV + i] = res;
-            __syncthreads();
-            double y = 0.0;
-            if (i < k)
-                for (int q = 0; q <= i; ++q) y = fma(S[L.TT + i * L.TS + q], S[L.VV + q], y);
-            S[L.LV + i] = y;
-            __syncthreads();
-            double dl = 0.0;
-            if (i < k)
-                for (int q = i; q < k; ++q) dl = fma(S[L.TT + q * L.TS + i], S[L.LV + q], dl);
-            lam += dl;
-            S[L.RV + i] = i < k ? sgn * dl : 0.0;
-            __syncthreads();
+#pragma unroll 1
+    for (int j0 = 0; j0 < NQ; j0 += 8) { // chunks of 8 independent loads (entries past n are 0)
+        double rv[8], xx[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = rq[j0 + u];
+            xx[u] = xv[j0 + u];
         }
-        if (i < L.NX) {
-            double dx = 0.0;
-            if (i < n) {
-                for (int q = 0; q < k; ++q) {
-                    const int c = (int)S[L.AC + q];
-                    if (c < NJ + 6) dx = fma(S[L.RV + q], S[L.XT + c * L.QS + i], dx);
-                }
-            } else {
-                for (int q = 0; q < k; ++q) dx = fma(S[L.RV + q], fcoef(S, L, (int)S[L.AC + q], i - n), dx);
-                dx *= ieps;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = fma(rv[u], xx[u], s);
+    }
+    const double *fr = S + L.FFJ + (jrow ? ci : 0) * L.FS;
+    double sf = 0.0;
+#pragma unroll
+    for (int f = 0; f < 3 * kCMax; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
+    if (jrow) return s + sf;
+    if (wrow) return s;
+    return xv[n + ci - L.NJ - 6];
+}
+
+// Per-lane vector of active-slot values (T rows, T columns, Gamma columns of the active
+// set): in registers (KM static; dynamic writes by select) or one LDS row per lane, whose
+// dots load in chunks of 8 independent reads. Either way the loads of a dot issue back to
+// back instead of one dependent LDS round trip per term.
+template <int KM, bool REG>
+struct SlotVec;
+
+template <int KM>
+struct SlotVec<KM, true> {
+    double v[KM];
+    __device__ void bind(double *, int) {}
+    __device__ void zero_from(int c)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = (j >= c) ? 0.0 : v[j];
+    }
+    __device__ void zero_if(bool cond)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = cond ? 0.0 : v[j];
+    }
+    __device__ void put(int c, bool cond, double x) { v[c] = cond ? x : v[c]; } // c static after unrolling
+    __device__ void put_dyn(int c, bool cond, double x)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = (cond && j == c) ? x : v[j];
+    }
+    __device__ void load_if(bool cond, const double *src, int cnt)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double w = src[j];
+            v[j] = (cond && j < cnt) ? w : v[j];
+        }
+    }
+    __device__ void shift_down(int c, int cnt) // v[j] = v[j + 1] for c <= j < cnt - 1
+    {
+#pragma unroll
+        for (int j = 0; j + 1 < KM; ++j) v[j] = (j >= c && j + 1 < cnt) ? v[j + 1] : v[j];
+    }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double bj = b[j];
+            s = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s);
+        }
+        return s;
+    }
+};
+
+template <int KM>
+struct SlotVec<KM, false> {
+    double *p;
+    int cap;
+    __device__ void bind(double *row, int capacity)
+    {
+        p = row;
+        cap = capacity;
+    }
+    __device__ void zero_from(int c)
+    {
+        for (int j = c; j < cap; ++j) p[j] = 0.0;
+    }
+    __device__ void zero_if(bool cond)
+    {
+        if (cond)
+            for (int j = 0; j < cap; ++j) p[j] = 0.0;
+    }
+    __device__ void put(int c, bool cond, double x)
+    {
+        if (cond) p[c] = x;
+    }
+    __device__ void put_dyn(int c, bool cond, double x)
+    {
+        if (cond) p[c] = x;
+    }
+    __device__ void load_if(bool cond, const double *src, int cnt)
+    {
+        if (cond)
+            for (int j = 0; j < cnt; ++j) p[j] = src[j];
+    }
+    __device__ void shift_down(int c, int cnt)
+    {
+        for (int j = c; j + 1 < cnt; ++j) p[j] = p[j + 1];
+    }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int c0 = 0; c0 < cnt; c0 += 8) {
+            double pv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                pv[u] = p[c0 + u];
+                bv[u] = b[c0 + u];
             }
-            S[L.XV + i] = (pass == 0 ? (i < n ? S[L.X0 + i] : 0.0) : S[L.XV + i]) + dx;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
         }
+        return s;
     }
-    __syncthreads();
+};
+
+// value of v in lane `lane` (uniform), as a scalar broadcast (v_readlane, no LDS)
+__device__ __forceinline__ double bcast(double v, int lane)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
-template <int NQ, bool TR>
-__global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const ContactArgs a)
+// compact index of equality a (a < 6: dynamic feasibility rows, then the waist rows)
+__device__ __forceinline__ int eq_row(int a, int NJ) { return a < 6 ? a : NJ + a - 6; }
+
+template <int NQ, bool TR, int KMR>
+__global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel(const ContactArgs a)
 {
     constexpr int NRC = TR ? 40 : 16; // Gauss-Jordan right-hand sides per pass
     extern __shared__ __attribute__((aligned(16))) double S[];
@@ -202,6 +264,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
     const int cm = a.cmask[b];
     const bool qrow = i < n;
     const int ic = qrow ? i : n - 1;
+    WBQ_STAMP(0);
 
     // ------------------------------------------------------------------ 1. stage
     // unconditional buffer loads (clamped offsets, values selected afterwards): one HBM trip
@@ -246,7 +309,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
     for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = (qrow && rr < 6 * nc) ? jc[rr] : 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) jw[r] = qrow ? jw[r] : 0.0;
-    if (qrow) {
+    if (i < L.NJ) { // joint constraint rows (every joint with torque rows, else the 6 base rows)
 #pragma unroll
         for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = mrow[r];
 #pragma unroll
@@ -266,6 +329,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         if (it * 64 + i < 24 * (1 + nc)) S[L.PS + it * 64 + i] = pv[it];
     if (i < 6 * (1 + nc)) S[L.JD + i] = jd;
     __syncthreads();
+    WBQ_STAMP(1);
 
     // ------------------------------------------------- 2. task targets (one lane per row)
     // Cartesian acceleration task: b = Kp e - Kd J qd - Jdot qd (xdd_ref = 0, xd_ref = 0)
@@ -300,6 +364,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         for (int j = 0; j < NQ; ++j) S[L.HR + i * L.QS + j] = A[j];
     }
 
+    WBQ_STAMP(2);
     // ------------- 4. X = H_qq^-1 [M rows 0..NJ-1 | J_w^T | -g]: block Gauss-Jordan, H SPD
     bool notspd = false;
     for (int c0 = 0; c0 < L.NR; c0 += NRC) {
@@ -314,7 +379,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         for (int m = 0; m < NRC; ++m) {
             const int s = c0 + m;
             double v = 0.0;
-            if (s < L.NJ) v = S[L.AQJ + ic * L.QS + s];
+            if (s < L.NJ) v = S[L.AQJ + s * L.QS + (i < NQ ? i : 0)]; // M[s][i] = M[i][s]
             else if (s < L.NJ + 6) v = S[L.AQW + (s - L.NJ) * L.QS + (i < NQ ? i : 0)];
             else if (s == L.NJ + 6) v = mg;
             rhs[m] = qrow ? v : 0.0;
@@ -334,6 +399,7 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         S[L.XV + i] = x0;
     }
 
+    WBQ_STAMP(3);
     // ------------------------------------------ 5. Gamma row ci, activities, bounds
     const int ci = i;
     const int NJ = L.NJ, ME = L.ME;
@@ -394,17 +460,99 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
     }
     __syncthreads();
     if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
-    const bool cons_eq = kind == 1;
+    WBQ_STAMP(4);
 
     // ------------------------------------ 6. dual active set in constraint space
+    // Slot a (lane a < k) = a-th active row: act (compact row), sgn (normal = sgn * a_act),
+    // lam (its multiplier), aeq (an equality, never dropped), row a and column a of
+    // T = L^-1 (Gamma_AA = L L^T, signed normals). Lane j (constraint row j) keeps its
+    // activity s_j and GA_j[q] = Gamma[j][act_q].
+    constexpr bool SREG = !TR;      // without torque rows k <= 12 + 3 nc <= KMR: registers
+    constexpr int KM = TR ? 64 : KMR;
+    SlotVec<KM, SREG> Trow, Tcol, GA;
+    if constexpr (!SREG) {
+        Trow.bind(S + (i < L.NX ? L.TT + i * L.TS : L.DUM), L.NX);
+        Tcol.bind(S + (i < L.NX ? L.TC + i * L.TS : L.DUM), L.NX);
+        GA.bind(S + (ci < ME ? L.GA + ci * L.TS : L.DUM), L.NX);
+    }
+    Trow.zero_from(0);
+    Tcol.zero_from(0);
+    GA.zero_from(0);
     int status = notspd ? 3 : (a.limits_crossed ? 2 : 0);
     int iters = 0, k = 0;
     int act = 0;       // slot i < k: compact row
-    double sgn = 1.0;  // its sign (normal = sgn * a_act)
+    double sgn = 1.0;  // its sign
     double lam = 0.0;  // its multiplier
-    bool aeq = false;  // it is an equality (never dropped)
+    bool aeq = false;  // it is an equality
     bool onact = false; // lane ci: row ci is in the active set
-    int eqn = 0, rounds = 0;
+    int rounds = 0;
+    if (status == 0) {
+        // The 12 equality rows in one batch. Lane r < 12 holds row r of Gamma_EE; a
+        // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane
+        // c then forward-substitutes column c of T = L^-1 against the broadcast rows of L, and
+        // lambda_E = T^T T (e_E - s_E), s += Gamma[:, E] lambda_E.
+        const int er = eq_row(i < 12 ? i : 0, NJ);
+        double g[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) g[c] = (i < 12) ? S[L.GM + er * L.GS + eq_row(c, NJ)] : 0.0;
+        double gd = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) gd = (i == c) ? g[c] : gd;
+        const double dmx = imax<64>(gd);
+        bool sing = false;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+            const double dcc = bcast(g[c], c);
+            sing |= !(dcc > 1e-14 * dmx);
+            const double ilc = dcc > 0.0 ? frsq(dcc) : 0.0;
+            g[c] = (i > c) ? g[c] * ilc : ((i == c) ? dcc * ilc : g[c]); // L[r][c], r >= c
+#pragma unroll
+            for (int j = c + 1; j < 12; ++j) {
+                const double ljc = bcast(g[c], j);
+                if (i >= j) g[j] = fma(-g[c], ljc, g[j]);
+            }
+        }
+        double t[12]; // column i of T (lanes i < 12)
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            double acc = (i == r) ? 1.0 : 0.0;
+#pragma unroll
+            for (int q = 0; q < r; ++q) acc = fma(-bcast(g[q], r), t[q], acc);
+            const double lrr = bcast(g[r], r);
+            t[r] = (i < 12 && lrr > 0.0) ? acc / lrr : 0.0;
+        }
+        // column i of T to lane i's Tcol; rows through LDS (lane c writes T[r][c] into row r
+        // of the TT region: the LDS Trow itself, or scratch for the register Trow)
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            Tcol.put(r, i < 12, t[r]);
+            if (i < 12) S[L.TT + r * L.TS + i] = t[r];
+        }
+        const double ye = __shfl(lo - s_i, er); // e_E - s_E (every lane active: sources up to lane NJ + 5)
+        if (i < 12) S[L.VV + i] = ye;
+        __syncthreads();
+        if constexpr (SREG) Trow.load_if(i < 12, S + L.TT + (i < 12 ? i : 0) * L.TS, 12);
+        const double w = i < 12 ? Trow.dot(S + L.VV, 12) : 0.0;
+        S[L.LV + i] = w;
+        __syncthreads();
+        const double lm = i < 12 ? Tcol.dot(S + L.LV, 12) : 0.0; // lambda_E
+        S[L.RV + i] = lm;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            GA.put(q, kind != 0, kind != 0 ? S[L.GM + ci * L.GS + eq_row(q, NJ)] : 0.0);
+        if (kind != 0) s_i += GA.dot(S + L.RV, 12);
+        if (i < 12) {
+            act = er;
+            aeq = true;
+            lam = lm;
+        }
+        onact = ci < 6 || (ci >= NJ && ci < NJ + 6);
+        k = 12;
+        iters = 1;
+        if (sing) status = 3; // dependent equality rows: the spec's level 1 is ill-posed
+        __syncthreads();
+    }
     bool need_select = true, dirty = true;
     int cp = 0;
     double sgp = 1.0, bnd = 0.0, lamp = 0.0;
@@ -412,37 +560,71 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
     bool go = status == 0;
     while (go) {
         if (need_select) {
-            if (eqn < 12) { // equalities first, in order: dynamics, then waist
-                cp = eqn < 6 ? eqn : NJ + eqn - 6;
-                ++eqn;
-                const double sp = __shfl(s_i, cp);
-                bnd = __shfl(lo, cp);
-                sgp = (sp - bnd > 0.0) ? -1.0 : 1.0;
-            } else {
-                double v = -1.0;
-                if (kind == 2 && !onact) {
-                    const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
-                    const double viol = fmax(lo - s_i, s_i - hi);
-                    if (viol > tol) v = viol / nrm;
-                }
-                int pi = i;
-                iargmax<64>(v, pi);
-                if (!(v > 0.0)) {
-                    // no violated row: x is current unless steps were taken since the last
-                    // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on
-                    // the active set, and re-check every row with the exact activities
-                    if (!dirty || rounds >= 3) break;
-                    ++rounds;
-                    dirty = false;
-                    rebuild_refine(S, L, i, k, n, nf, act, sgn, lam, lo, hi, ieps);
-                    if (kind != 0) s_i = activity(S, L, ci, n, nf);
-                    continue;
-                }
-                cp = pi;
-                const double vl = __shfl(lo - s_i, cp), vh = __shfl(s_i - hi, cp);
-                sgp = vl > vh ? 1.0 : -1.0;
-                bnd = sgp > 0.0 ? __shfl(lo, cp) : __shfl(hi, cp);
+            double v = -1.0;
+            if (kind == 2 && !onact) {
+                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                const double viol = fmax(lo - s_i, s_i - hi);
+                if (viol > tol) v = viol / nrm;
             }
+            int pi = i;
+            iargmax<64>(v, pi);
+            if (!(v > 0.0)) {
+                // no violated row: x is current unless steps were taken since the last
+                // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on the
+                // active set, and re-check every row with the exact activities
+                if (!dirty || rounds >= 3) break;
+                ++rounds;
+                dirty = false;
+                const double lo_a = __shfl(lo, act), hi_a = __shfl(hi, act); // all lanes active
+                S[L.RV + i] = i < k ? sgn * lam : 0.0;
+                S[L.AC + i] = (double)act;
+                __syncthreads();
+                for (int pass = 0; pass < 3; ++pass) {
+                    if (pass > 0) {
+                        // residual of the active rows, exact in x-space; correction through T
+                        const double res = i < k ? sgn * ((sgn > 0.0 ? lo_a : hi_a) - activity<NQ>(S, L, act, n, nf)) : 0.0;
+                        S[L.VV + i] = res;
+                        __syncthreads();
+                        const double y = Trow.dot(S + L.VV, k);
+                        S[L.LV + i] = i < k ? y : 0.0;
+                        __syncthreads();
+                        const double dl = i < k ? Tcol.dot(S + L.LV, k) : 0.0;
+                        lam += dl;
+                        S[L.RV + i] = i < k ? sgn * dl : 0.0;
+                        __syncthreads();
+                    }
+                    if (i < L.NX) { // x += H^-1 A_A^T (sgn dlam), slots in chunks of 8 loads
+                        double dx = 0.0;
+                        const int fi = i - n;
+                        for (int q0 = 0; q0 < k; q0 += 8) {
+                            int cq[8];
+                            double wq[8], xq[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                cq[u] = q0 + u < k ? (int)S[L.AC + q0 + u] : 0;
+                                wq[u] = q0 + u < k ? S[L.RV + q0 + u] : 0.0;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int c = cq[u] < NJ + 6 ? cq[u] : 0;
+                                xq[u] = i < n ? (cq[u] < NJ + 6 ? S[L.XT + c * L.QS + i] : 0.0)
+                                              : fcoef(S, L, cq[u], fi < 0 ? 0 : fi);
+                            }
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) dx = fma(wq[u], xq[u], dx);
+                        }
+                        if (i >= n) dx *= ieps;
+                        S[L.XV + i] = (pass == 0 ? (i < n ? S[L.X0 + i] : 0.0) : S[L.XV + i]) + dx;
+                    }
+                    __syncthreads();
+                }
+                if (kind != 0) s_i = activity<NQ>(S, L, ci, n, nf);
+                continue;
+            }
+            cp = pi;
+            const double vl = __shfl(lo - s_i, cp), vh = __shfl(s_i - hi, cp);
+            sgp = vl > vh ? 1.0 : -1.0;
+            bnd = sgp > 0.0 ? __shfl(lo, cp) : __shfl(hi, cp);
             lamp = 0.0;
         }
         if (++iters > maxit) {
@@ -452,26 +634,17 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         dirty = true;
         // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
         const double gpp = S[L.GM + cp * L.GS + cp];
-        if (i < k) S[L.VV + i] = sgn * sgp * S[L.GM + act * L.GS + cp];
+        S[L.VV + i] = i < k ? sgn * sgp * S[L.GM + act * L.GS + cp] : 0.0;
         __syncthreads();
-        double l = 0.0;
-        if (i < k)
-            for (int q = 0; q <= i; ++q) l = fma(S[L.TT + i * L.TS + q], S[L.VV + q], l);
+        const double l = i < k ? Trow.dot(S + L.VV, k) : 0.0;
         S[L.LV + i] = l;
         __syncthreads();
-        double r = 0.0;
-        if (i < k)
-            for (int q = i; q < k; ++q) r = fma(S[L.TT + q * L.TS + i], S[L.LV + q], r);
+        const double r = i < k ? Tcol.dot(S + L.LV, k) : 0.0;
         const double d2 = gpp - isum<64>(l * l);
         S[L.RV + i] = i < k ? sgn * r : 0.0;
-        S[L.AC + i] = (double)act;
         __syncthreads();
-        double ds = 0.0;
-        if (kind != 0) {
-            const double *gr = S + L.GM + ci * L.GS;
-            ds = sgp * gr[cp];
-            for (int q = 0; q < k; ++q) ds = fma(-gr[(int)S[L.AC + q]], S[L.RV + q], ds);
-        }
+        const double gjp = (kind != 0) ? S[L.GM + ci * L.GS + cp] : 0.0;
+        const double ds = (kind != 0) ? sgp * gjp - GA.dot(S + L.RV, k) : 0.0;
         const double zz = sgp * __shfl(ds, cp);
         const double slack = sgp * (__shfl(s_i, cp) - bnd); // < 0: violated
         const double rmax = imax<64>(i < k ? fabs(r) : 0.0);
@@ -480,30 +653,31 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         iargmin<64>(cand, blk);
         const double t1 = cand;
         const double t2 = (zz > 1e-14 * gpp) ? -slack / zz : kInf;
-        const bool peq = __shfl(cons_eq ? 1 : 0, cp) != 0;
         if (t1 >= kInf && t2 >= kInf) {
-            if (peq && fabs(slack) <= 1e-10 * fmax(1.0, fabs(bnd))) { // dependent, consistent
-                need_select = true;
-                __syncthreads();
-                continue;
-            }
             status = 2; // no feasible point with level 0 at b_w (level-0 repair: next)
+            break;
+        }
+        if (t2 <= t1 && k >= KM) { // cannot happen for independent rows; guard the storage
+            status = 3;
             break;
         }
         const double t = fmin(t1, t2);
         s_i = fma(t, ds, s_i);
         if (i < k) lam = fma(-t, r, lam);
         lamp += t;
-        if (t2 <= t1) { // add cp
-            const double dd = d2 > 0.0 ? d2 : zz;
-            const double id = frsq(dd);
-            if (i < k) S[L.TT + k * L.TS + i] = -r * id;
+        if (t2 <= t1) { // add cp: T row k = [-(T^T l)^T / d, 1/d]
+            const double id = frsq(d2 > 0.0 ? d2 : zz);
+            const double tk = i < k ? -r * id : (i == k ? id : 0.0);
+            Tcol.put_dyn(k, i <= k, tk);
+            GA.put_dyn(k, kind != 0, gjp);
+            S[L.WV + i] = tk;
+            __syncthreads();
+            Trow.load_if(i == k, S + L.WV, k + 1);
             if (i == k) {
-                S[L.TT + k * L.TS + k] = id;
                 act = cp;
                 sgn = sgp;
                 lam = lamp;
-                aeq = peq;
+                aeq = false;
             }
             if (i == cp) onact = true;
             ++k;
@@ -521,22 +695,57 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
                 lam = nl;
                 aeq = ne;
             }
+            GA.shift_down(blk, k);
             --k;
+            // rows and columns of T before blk stand; re-append the slots after it
+            Trow.zero_if(i >= blk);
+            Tcol.zero_from(blk);
             __syncthreads();
-            for (int a2 = blk; a2 < k; ++a2) // rows before blk of T stand; re-append the rest
-                (void)t_append(S, L, i, a2, __shfl(act, a2), __shfl(sgn, a2), act, sgn);
+            for (int a2 = blk; a2 < k; ++a2) {
+                const int cq = __shfl(act, a2);
+                const double sq = __shfl(sgn, a2);
+                S[L.VV + i] = i < a2 ? sgn * sq * S[L.GM + act * L.GS + cq] : 0.0;
+                __syncthreads();
+                const double l2 = i < a2 ? Trow.dot(S + L.VV, a2) : 0.0;
+                S[L.LV + i] = l2;
+                __syncthreads();
+                const double r2 = i < a2 ? Tcol.dot(S + L.LV, a2) : 0.0;
+                const double e2 = S[L.GM + cq * L.GS + cq] - isum<64>(l2 * l2);
+                const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
+                const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
+                Tcol.put_dyn(a2, i <= a2, tk2);
+                S[L.WV + i] = tk2;
+                __syncthreads();
+                Trow.load_if(i == a2, S + L.WV, a2 + 1);
+                __syncthreads();
+            }
             need_select = false;
         }
     }
 
     // ------------------------------------------------------------------ 7. outputs
     __syncthreads();
+    WBQ_STAMP(5);
     const bool ok = status == 0;
     double tau_i = h_i;
     if (ok && qrow) { // joint row i: M_i qdd - J_c,i^T f + h_i
         double t = h_i;
-        for (int j = 0; j < n; ++j) t = fma(S[L.AQJ + i * L.QS + j], S[L.XV + j], t);
-        for (int f = 0; f < nf; ++f) t = fma(S[L.FFJ + i * L.FS + f], S[L.XV + n + f], t);
+        // lane i's own M row and contact-Jacobian column, re-read (L2) rather than held
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
+        const int moff = (int)(8 * (b * n * n + ic));
+        double mr[NQ], jr[3 * kCMax]; // unconditional (clamped) loads: one round trip
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) mr[j] = bload(Mrs, moff, 8 * (j < n ? j : n - 1) * n);
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.Jc, Bn * nc * 6);
+        const int joff = (int)(8 * (b * nc * 6 * n + ic));
+#pragma unroll
+        for (int f = 0; f < 3 * kCMax; ++f)
+            jr[f] = bload(Jrs, joff, 8 * (6 * (f < nf ? f / 3 : 0) + f % 3) * n);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) t = fma(j < n ? mr[j] : 0.0, S[L.XV + (j < n ? j : 0)], t);
+#pragma unroll
+        for (int f = 0; f < 3 * kCMax; ++f)
+            t = fma((f < nf && ((cm >> (f / 3)) & 1)) ? -jr[f] : 0.0, S[L.XV + n + (f < nf ? f : 0)], t);
         tau_i = t;
     }
     const double tmax = imax<64>((qrow && !isfinite(tau_i)) ? 1.0 : 0.0);
@@ -548,24 +757,36 @@ __global__ __launch_bounds__(64, NQ == 32 ? 2 : 1) void contact_kernel(const Con
         a.status[b] = status;
         a.iters[b] = iters;
     }
+    WBQ_STAMP(6);
+#ifdef WBQ_STAMPS
+    if (i == 0 && a.stamps) a.stamps[b * kStamps + 7] = rounds;
+#endif
 }
 
-template <int NQ, bool TR>
+template <int NQ, bool TR, int KMR>
 hipError_t launch_t(const ContactArgs &a, hipStream_t stream)
 {
     constexpr int NRC = TR ? 40 : 16;
     static size_t attr = 0;
     const ContactLayout L(a.n, a.nc, TR, NQ, NRC);
     if (L.NR > NRC * ((NQ == 64 && TR) ? 2 : 1) || L.ME > 64 || L.NX > 64) return hipErrorInvalidValue;
+    if (!TR && L.ME > KMR) return hipErrorInvalidValue; // the register slot vectors hold every active row
     const size_t lds = sizeof(double) * L.SIZE;
     if (lds > attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)contact_kernel<NQ, TR>,
+        hipError_t e = hipFuncSetAttribute((const void *)contact_kernel<NQ, TR, KMR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = lds;
     }
-    hipLaunchKernelGGL((contact_kernel<NQ, TR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     return hipGetLastError();
+}
+
+template <int NQ>
+hipError_t launch_nq(const ContactArgs &a, hipStream_t stream)
+{
+    if (a.torque_rows) return launch_t<NQ, true, 64>(a, stream);
+    return a.nc <= 2 ? launch_t<NQ, false, 18>(a, stream) : launch_t<NQ, false, 24>(a, stream);
 }
 
 }  // namespace
@@ -580,8 +801,7 @@ size_t contact_lds_bytes(int n, int nc, int torque_rows)
 hipError_t launch_contact(const ContactArgs &a, hipStream_t stream)
 {
     if (a.B <= 0) return hipSuccess;
-    if (a.n <= 32) return a.torque_rows ? launch_t<32, true>(a, stream) : launch_t<32, false>(a, stream);
-    return a.torque_rows ? launch_t<64, true>(a, stream) : launch_t<64, false>(a, stream);
+    return a.n <= 32 ? launch_nq<32>(a, stream) : launch_nq<64>(a, stream);
 }
 
 }  // namespace wbq

@@ -161,6 +161,7 @@ int solve_contact(wbq_ctx *c)
     a.status = c->out_status ? c->out_status : c->status;
     a.iters = c->out_iters ? c->out_iters : c->iters;
     a.x = c->dev_x;
+    a.stamps = c->stamps;
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
                        (c->solves++ % (unsigned long long)c->timing_every) == 0;
@@ -320,6 +321,10 @@ int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
     ok = hipMemcpy(c->tmax, tmx.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
          hipMemcpy(c->tmin, tmn.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
+#ifdef WBQ_STAMPS
+    if (hipMalloc(&c->stamps, sizeof(unsigned long long) * wbq::kStamps * B) != hipSuccess)
+        return cleanup(WBQ_E_DEVICE);
+#endif
     *out = c;
     return WBQ_SUCCESS;
 }

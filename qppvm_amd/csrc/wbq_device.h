@@ -8,6 +8,19 @@ namespace wbq {
 
 constexpr double kInf = 1.0e300;
 
+// Phase stamps for the diagnostic build only (never compiled into the product library).
+#ifdef WBQ_STAMPS
+#define WBQ_STAMP(k)                                                                    \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                     \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (threadIdx.x == 0 && a.stamps) a.stamps[blockIdx.x * kStamps + (k)] = t_;    \
+    } while (0)
+#else
+#define WBQ_STAMP(k) do {} while (0)
+#endif
+
 // fast reciprocal / reciprocal square root: hardware estimate + one Newton step (~0.5 ulp)
 __device__ __forceinline__ double frcp(double x)
 {

@@ -80,6 +80,7 @@ struct ContactArgs {
     double *x;       // [B][n + 3 nc]
     int *status;     // [B]
     int *iters;      // [B]
+    unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [B][kStamps] s_memtime
 };
 
 hipError_t launch_contact(const ContactArgs &a, hipStream_t stream);
