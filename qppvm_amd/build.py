@@ -42,27 +42,31 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
 
 PLUGIN_DIR = os.path.join(HERE, "plugins")
 PLUGIN_LIB = os.path.join(HERE, "libQPPVMPlugin.so")
+FORCEACC_LIB = os.path.join(HERE, "libForceAccPlugin.so")
 DRIVER = os.path.join(HERE, "qppvm_dummy_driver")
 
 
 def build_plugins(verbose: bool = False) -> tuple:
-    """The XBot plugin shell (libQPPVMPlugin.so, same target name as the reference's
-    CMakeLists.txt:48) and the config-0 dummy-mode driver, host C++ over libwbq.so."""
+    """The XBot plugin shells (libQPPVMPlugin.so and libForceAccPlugin.so, the reference's
+    target names, CMakeLists.txt:48-49) and the config-0 dummy-mode driver, host C++ over
+    libwbq.so."""
     build()
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(PLUGIN_DIR, "compat"),
            "-I", os.path.join(PLUGIN_DIR, "include"), "-I", os.path.join(PLUGIN_DIR, "src")]
     link = ["-L", HERE, "-lwbq", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"]
     src = os.path.join(PLUGIN_DIR, "src", "QPPVMPlugin.cpp")
+    fsrc = os.path.join(PLUGIN_DIR, "src", "ForceAcc.cpp")
     cmds = [
         ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", *inc, src, "-o", PLUGIN_LIB, *link],
-        ["g++", "-O2", "-std=c++17", "-Wall", *inc, os.path.join(PLUGIN_DIR, "src", "dummy_driver.cpp"), src,
+        ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", *inc, fsrc, "-o", FORCEACC_LIB, *link],
+        ["g++", "-O2", "-std=c++17", "-Wall", *inc, os.path.join(PLUGIN_DIR, "src", "dummy_driver.cpp"), src, fsrc,
          "-o", DRIVER, *link],
     ]
     for c in cmds:
         if verbose:
             print(" ".join(c), file=sys.stderr)
         subprocess.check_call(c)
-    return PLUGIN_LIB, DRIVER
+    return PLUGIN_LIB, DRIVER, FORCEACC_LIB
 
 
 if __name__ == "__main__":

@@ -7,7 +7,8 @@
 //                         getMotorPosition/Velocity, setReferenceFrom, move
 //   XBot::ModelInterface: getJointNum, update, computeNonlinearTerm, getEffortLimits,
 //                         getRobotState, set/getJointPosition, set/getJointVelocity,
-//                         setJointEffort, getPose, getJacobian, getInertiaMatrix
+//                         setJointEffort, getPose, getJacobian, getInertiaMatrix,
+//                         computeJdotQdot, getPointPosition
 //   REGISTER_XBOT_PLUGIN(name, class) -> extern "C" factory symbols
 // Building against the real XCM is an install-time swap of this include directory; the
 // linear-algebra types below stand in for Eigen's (row-major, fp64).
@@ -107,6 +108,22 @@ public:
     virtual bool getPose(const std::string &link, Eigen::Affine3d &w_T_link) const = 0;
     virtual bool getJacobian(const std::string &link, Eigen::MatrixXd &J) const = 0;
     virtual bool getInertiaMatrix(Eigen::MatrixXd &M) const = 0;
+    // used by the ForceAcc plugin (XBotInterface: computeJdotQdot(link, point, jdotqdot) and
+    // getPointPosition(link, point, p), here at the link origin)
+    virtual bool computeJdotQdot(const std::string &link, Eigen::VectorXd &jdqd) const
+    {
+        (void)link;
+        jdqd.setZero(6);
+        return true;
+    }
+    virtual bool getPointPosition(const std::string &link, Eigen::VectorXd &p) const
+    {
+        Eigen::Affine3d T;
+        if (!getPose(link, T)) return false;
+        p.setZero(3);
+        for (int k = 0; k < 3; ++k) p[k] = T.m[4 * k + 3];
+        return true;
+    }
 };
 
 class Handle {

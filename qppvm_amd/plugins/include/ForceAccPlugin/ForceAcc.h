@@ -1,0 +1,66 @@
+// ForceAcc.h -- drop-in XBotPlugin::ForceAccExample on the MI355X batched WBC-QP engine.
+//
+// Same class, namespace and XBot surface as the reference
+// (include/ForceAccPlugin/ForceAcc.h:30-53): init_control_plugin, close, on_start, on_stop,
+// protected control_loop. What the reference builds from OpenSoT (OptvarHelper variables
+// qddot + 3 force components per foot, acceleration::Cartesian feet/waist tasks, Postural,
+// DynamicFeasibility, wrench bounds, AutoStack, QPOases_sot) and the inverse-dynamics post-step
+// go through the wbq contact-form C ABI (include/wbq.h, wbq_create_contact); one context per
+// plugin, allocated in init_control_plugin.
+#pragma once
+
+#include <XCM/XBotControlPlugin.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "wbq.h"
+
+namespace XBotPlugin {
+
+class ForceAccExample : public XBot::XBotControlPlugin {
+public:
+    bool init_control_plugin(XBot::Handle::Ptr handle) override;
+    bool close() override;
+    void on_start(double time) override;
+    void on_stop(double time) override {}
+    ~ForceAccExample() override;
+
+    // observability (the reference logs tau, tau_c, qddot_value, x and the wrenches)
+    const Eigen::VectorXd &tau() const { return _tau; }
+    const Eigen::VectorXd &x() const { return _x; }
+    const Eigen::VectorXd &qddot_value() const { return _qddot_value; }
+    int last_status() const { return _status; }
+    int solver_errors() const { return _solver_errors; }
+    // the per-tick solver inputs of the last control_loop (dumped by the dummy driver)
+    const std::vector<double> &staged(int field) const { return _in[field]; }
+    int contact_mask() const { return _cmask; }
+
+protected:
+    void control_loop(double time, double period) override;
+
+private:
+    void sync_model();
+
+    XBot::RobotInterface::Ptr _robot;
+    XBot::ModelInterface::Ptr _model;
+    wbq_ctx *_ctx = nullptr;
+
+    double _start_time = 0.0;
+    int _status = 0;
+    int _solver_errors = 0;
+    int _cmask = 0xF;
+
+    Eigen::VectorXd _k, _d, _q, _qdot, _q_ref, _tau, _x, _qddot_value, _h;
+    Eigen::VectorXd _initial_com;
+    Eigen::Affine3d _waist_ref;
+    std::vector<Eigen::Affine3d> _feet_ref;
+    std::vector<std::string> _contact_links{"foot_fl", "foot_fr", "foot_hr", "foot_hl"}; // ForceAcc.cpp:58
+    std::string _waist_link = "pelvis";                                                   // :29
+    // staged wbq_contact_inputs fields (M, h, q, qd, qref, Jw, jdqd_w, pose_w, pose_w_ref,
+    // Jc, jdqd_c, pose_c, pose_c_ref), one instance
+    std::vector<double> _in[13];
+};
+
+}  // namespace XBotPlugin

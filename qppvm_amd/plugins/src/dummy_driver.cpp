@@ -1,7 +1,9 @@
-// dummy_driver.cpp -- BASELINE config 0: the QPPVM plugin in an XBotCore-like dummy loop.
+// dummy_driver.cpp -- BASELINE config 0: a plugin in an XBotCore-like dummy loop.
 // init_control_plugin -> on_start -> N x control_loop (period 1 ms) -> close, on the
-// synthetic robot of dummy_robot.h. Reports us/tick; optionally dumps the first ticks'
-// solver inputs and torques (binary, for the oracle parity test).
+// synthetic robots of dummy_robot.h: the QPPVM plugin (default, n = 39 arms robot) or, with
+// --plugin forceacc, the ForceAcc plugin on a floating-base quadruped (n = 30, 4 feet).
+// Reports us/tick; optionally dumps the first ticks' solver inputs and outputs (binary, for
+// the oracle parity tests).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -9,22 +11,79 @@
 #include <memory>
 #include <string>
 
+#include <ForceAccPlugin/ForceAcc.h>
 #include <QPPVM_RT_plugin/QPPVMPlugin.h>
 
 #include "dummy_robot.h"
 
+// ForceAcc in dummy mode: dump = header (n, nc, ticks), then per tick the 13 staged solver
+// input fields, the contact mask, tau, x and the status
+static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
+{
+    auto handle = std::make_shared<dummy::Handle>(dummy::quadruped(n));
+    XBotPlugin::ForceAccExample plugin;
+    if (!plugin.init_control_plugin(handle)) {
+        std::fprintf(stderr, "init_control_plugin failed\n");
+        return 2;
+    }
+    FILE *f = dump ? std::fopen(dump, "wb") : nullptr;
+    const double dt = 1e-3;
+    {
+        Eigen::VectorXd q(n, 0.0), qd(n, 0.0);
+        for (int j = 0; j < n; ++j) qd[j] = 0.1 * ((j % 5) - 2);
+        handle->robot().set_state(q, qd);
+    }
+    plugin.on_start(0.0);
+    const int nc = 4;
+    if (f) {
+        const int hdr[3] = {n, nc, dump_ticks};
+        std::fwrite(hdr, sizeof(int), 3, f);
+    }
+    double worst = 0.0, run_total = 0.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < ticks; ++k) {
+        const auto a = std::chrono::steady_clock::now();
+        plugin.run((k + 1) * dt, dt);
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+        worst = us > worst ? us : worst;
+        run_total += us;
+        if (f && k < dump_ticks) {
+            for (int fld = 0; fld < 13; ++fld)
+                std::fwrite(plugin.staged(fld).data(), sizeof(double), plugin.staged(fld).size(), f);
+            const int cm = plugin.contact_mask(), st = plugin.last_status();
+            std::fwrite(&cm, sizeof(int), 1, f);
+            std::fwrite(plugin.tau().data(), sizeof(double), n, f);
+            std::fwrite(plugin.x().data(), sizeof(double), n + 3 * nc, f);
+            std::fwrite(&st, sizeof(int), 1, f);
+        }
+        // dummy-mode kinematics with the QP's acceleration (ForceAcc.cpp:225-226)
+        handle->robot().step_qdd(plugin.qddot_value(), dt);
+    }
+    const double total = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (f) std::fclose(f);
+    plugin.close();
+    std::printf("{\"config\": 0, \"plugin\": \"ForceAccExample\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
+                "\"run_us\": %.3f, \"worst_us\": %.3f, \"solver_errors\": %d}\n", n, ticks, total / ticks,
+                run_total / ticks, worst, plugin.solver_errors());
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
-    int ticks = 10000, dump_ticks = 0, n = 39;
+    int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
+    bool forceacc = false;
     for (int k = 1; k < argc; ++k) {
         if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
         else if (!std::strcmp(argv[k], "--n") && k + 1 < argc) n = std::atoi(argv[++k]);
+        else if (!std::strcmp(argv[k], "--plugin") && k + 1 < argc) forceacc = !std::strcmp(argv[++k], "forceacc");
         else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
             dump = argv[++k];
             dump_ticks = std::atoi(argv[++k]);
         }
     }
+    if (forceacc) return run_forceacc(ticks, n > 0 ? n : 30, dump, dump_ticks);
+    if (n <= 0) n = 39;
     dummy::Params prm;
     prm.n = n;
     auto handle = std::make_shared<dummy::Handle>(prm);
@@ -97,7 +156,7 @@ int main(int argc, char **argv)
     plugin.close();
     // us_per_tick: the whole loop (plugin tick + dummy model + physics); run_us: the plugin
     // tick alone (model queries, one wbq solve, torque write-back)
-    std::printf("{\"config\": 0, \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, \"run_us\": %.3f, "
+    std::printf("{\"config\": 0, \"plugin\": \"QPPVMPlugin\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, \"run_us\": %.3f, "
                 "\"worst_us\": %.3f, \"solver_errors\": %d}\n", n, ticks, total / ticks, run_total / ticks, worst,
                 plugin.solver_errors());
     return 0;

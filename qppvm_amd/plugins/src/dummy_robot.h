@@ -17,11 +17,26 @@ namespace dummy {
 struct Params {
     int n = 39;
     unsigned seed = 7;
+    // links with a Jacobian / pose: QPPVM's end effectors (default), or a floating-base
+    // quadruped (pelvis + 4 feet) for the ForceAcc plugin
+    std::vector<std::string> links{"arm2_7", "arm1_7"};
+    bool floating_base = false; // first 6 coordinates = floating base; gravity on its z row
 };
+
+inline Params quadruped(int n = 30)
+{
+    Params p;
+    p.n = n;
+    p.seed = 11;
+    p.links = {"pelvis", "foot_fl", "foot_fr", "foot_hr", "foot_hl"};
+    p.floating_base = true;
+    return p;
+}
 
 class Model : public XBot::ModelInterface {
 public:
-    explicit Model(const Params &p) : n_(p.n), q_(p.n, 0.0), qd_(p.n, 0.0), tau_(p.n, 0.0)
+    explicit Model(const Params &p)
+        : n_(p.n), links_(p.links), fb_(p.floating_base), q_(p.n, 0.0), qd_(p.n, 0.0), tau_(p.n, 0.0)
     {
         std::mt19937_64 g(p.seed);
         std::normal_distribution<double> N(0.0, 1.0);
@@ -42,10 +57,20 @@ public:
         }
         lam_.resize(n_);
         for (auto &l : lam_) l = std::exp(std::log(0.1) + U(g) * std::log(100.0)); // cond ~ 1e2
-        for (int t = 0; t < 2; ++t) {
-            J0_[t].assign((size_t)6 * n_, 0.0);
+        const int nl = (int)links_.size();
+        J0_.assign(nl, std::vector<double>((size_t)6 * n_, 0.0));
+        p0_.assign(nl, std::vector<double>(3, 0.0));
+        for (int t = 0; t < nl; ++t) {
             for (auto &v : J0_[t]) v = 0.5 * N(g);
-            for (int k = 0; k < 3; ++k) p0_[t][k] = (t == 0 ? -0.4 : 0.4) * (k == 1) + 0.5 * (k == 2);
+            if (fb_ && t == 0) { // the base link moves with the floating base only
+                for (auto &v : J0_[t]) v = 0.0;
+                for (int r = 0; r < 6; ++r) J0_[t][r * n_ + r] = 1.0;
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 3; c < 6; ++c) J0_[t][r * n_ + c] = 0.2 * N(g);
+            }
+            for (int k = 0; k < 3; ++k)
+                p0_[t][k] = fb_ ? (t == 0 ? (k == 2 ? 0.6 : 0.0) : 0.4 * (k == 0 ? ((t & 1) ? 1 : -1) : (k == 1 ? (t < 3 ? 1 : -1) : 0)))
+                                : (t == 0 ? -0.4 : 0.4) * (k == 1) + 0.5 * (k == 2);
         }
         psi_.resize(n_);
         for (auto &v : psi_) v = 6.28 * U(g);
@@ -56,6 +81,7 @@ public:
     {
         h.setZero(n_);
         for (int j = 0; j < n_; ++j) h[j] = 10.0 * std::sin(q_[j] + psi_[j]) + 0.5 * qd_[j];
+        if (fb_) h[2] += 50.0; // gravity on the base z row: the feet must push up
         return true;
     }
     bool getEffortLimits(Eigen::VectorXd &tmax) const override { tmax.setConstant(n_, 150.0); return true; }
@@ -88,6 +114,15 @@ public:
             for (int c = 0; c < n_; ++c) J(r, c) = J0_[t][r * n_ + c] * (1.0 + 0.1 * std::cos(q_[c]));
         return true;
     }
+    // d/dt (J) qd with J_rc = J0_rc (1 + 0.1 cos q_c): sum_c -0.1 J0_rc sin(q_c) qd_c^2
+    bool computeJdotQdot(const std::string &link, Eigen::VectorXd &jdqd) const override
+    {
+        const int t = task(link);
+        jdqd.setZero(6);
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < n_; ++c) jdqd[r] -= 0.1 * J0_[t][r * n_ + c] * std::sin(q_[c]) * qd_[c] * qd_[c];
+        return true;
+    }
     bool getPose(const std::string &link, Eigen::Affine3d &T) const override
     {
         const int t = task(link);
@@ -117,11 +152,17 @@ public:
     const std::vector<double> &effort() const { return tau_; }
 
 private:
-    static int task(const std::string &link) { return link == "arm1_7" ? 1 : 0; }
+    int task(const std::string &link) const
+    {
+        for (size_t t = 0; t < links_.size(); ++t)
+            if (links_[t] == link) return (int)t;
+        return 0;
+    }
     int n_;
+    std::vector<std::string> links_;
+    bool fb_;
     std::vector<double> q_, qd_, tau_, Q_, lam_, psi_;
-    std::vector<double> J0_[2];
-    double p0_[2][3];
+    std::vector<std::vector<double>> J0_, p0_;
 };
 
 class Robot : public XBot::RobotInterface {
@@ -150,6 +191,15 @@ public:
     }
     bool move() override { return true; }
     void set_state(const Eigen::VectorXd &q, const Eigen::VectorXd &qd) { q_ = q; qd_ = qd; }
+    // dummy-mode kinematic step with a given acceleration (the integration the reference
+    // leaves commented out at ForceAcc.cpp:225-226): semi-implicit Euler
+    void step_qdd(const Eigen::VectorXd &qdd, double dt)
+    {
+        for (int j = 0; j < n_; ++j) {
+            qd_[j] += dt * qdd[j];
+            q_[j] += dt * qd_[j];
+        }
+    }
     // dummy-mode physics: q'' = M^-1 (tau - h), semi-implicit Euler
     void step(const Model &model, double dt)
     {
@@ -201,9 +251,9 @@ private:
 class Handle : public XBot::Handle {
 public:
     explicit Handle(const Params &p) : model_(std::make_shared<Model>(p)), robot_(std::make_shared<Robot>(p.n)) {}
+    std::string getPathToConfigFile() const override { return "dummy://synthetic"; }
     XBot::RobotInterface::Ptr getRobotInterface() override { return robot_; }
     XBot::ModelInterface::Ptr getModel() override { return model_; }
-    std::string getPathToConfigFile() const override { return "dummy://centauro-like"; }
     Model &model() { return *model_; }
     Robot &robot() { return *robot_; }
 

@@ -29,4 +29,5 @@ fi
 if [ "$STEPS" = "all" ] || [ "$STEPS" = "plugin" ]; then
   cd "$GRAFT_REPO_ROOT"
   run dummy_driver 300 ./qppvm_amd/qppvm_dummy_driver --ticks 10000 --dump gpurun_out/dummy_dump.bin 50 || exit 1
+  run dummy_driver_forceacc 300 ./qppvm_amd/qppvm_dummy_driver --plugin forceacc --ticks 10000 || exit 1
 fi

@@ -82,3 +82,15 @@ def test_unsupported_problem_rejected_before_device(lib):
     assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_UNSUPPORTED
     d.form, d.n = wbq.FORM_QPPVM, 65  # n too large
     assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_INVALID
+
+
+def test_plugin_shells_export_factories():
+    """libQPPVMPlugin.so / libForceAccPlugin.so (the reference's target names,
+    CMakeLists.txt:48-49) build with g++ against the compat XCM header and export the
+    REGISTER_XBOT_PLUGIN factory symbols XBotCore dlopens."""
+    plugin, driver, forceacc = wbq_build.build_plugins()
+    for lib, cls in ((plugin, "QPPVMPlugin"), (forceacc, "ForceAccExample")):
+        out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+        for sym in (f"create_instance_{cls}", f"destroy_instance_{cls}"):
+            assert re.search(rf"\bT {sym}$", out, re.M), (lib, sym)
+    assert os.access(driver, os.X_OK)

@@ -1,4 +1,5 @@
-"""BASELINE config 0 end to end: the XBot plugin shell (QPPVMPlugin over the C ABI) driven by
+"""BASELINE config 0 end to end: the XBot plugin shells (QPPVMPlugin, ForceAccExample over the
+C ABI) driven by
 the dummy-mode loop on the synthetic n = 39 robot. The driver dumps each tick's solver
 inputs and the torque the plugin applied; the oracle re-solves every dumped tick
 (tolerance 1e-6 relative, statuses equal). With 150 Nm limits most ticks are level-0
@@ -41,7 +42,7 @@ def read_dump(path):
 
 def test_dummy_driver_matches_oracle(tmp_path, oracle_lib):
     from qppvm_amd import build
-    _, driver = build.build_plugins()
+    driver = build.build_plugins()[1]
     dump = str(tmp_path / "dump.bin")
     r = subprocess.run([driver, "--ticks", "300", "--dump", dump, "40"], capture_output=True, text=True,
                        timeout=240)
@@ -50,6 +51,51 @@ def test_dummy_driver_matches_oracle(tmp_path, oracle_lib):
     prob = QPPVMProblem(n=n, tau_max=150.0)
     inp = {k: np.ascontiguousarray(d[k]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
     tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+    np.testing.assert_array_equal(d["status"], st_r)
+    ok = st_r == 0
+    assert ok.sum() >= len(ok) - 2
+    assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, rel_err(d["tau"][ok], tau_r[ok])
+
+
+def read_forceacc_dump(path):
+    raw = open(path, "rb").read()
+    n, nc, ticks = (int(v) for v in np.frombuffer(raw[:12], dtype=np.int32))
+    off = 12
+    shapes = {"M": (n, n), "h": (n,), "q": (n,), "qd": (n,), "qref": (n,), "Jw": (6, n), "jdqd_w": (6,),
+              "pose_w": (12,), "pose_w_ref": (12,), "Jc": (nc, 6, n), "jdqd_c": (nc, 6), "pose_c": (nc, 12),
+              "pose_c_ref": (nc, 12)}
+    rec = {k: [] for k in list(shapes) + ["cmask", "tau", "x", "status"]}
+    for _ in range(ticks):
+        for k, shp in shapes.items():
+            cnt = int(np.prod(shp))
+            rec[k].append(np.frombuffer(raw[off:off + 8 * cnt], dtype=np.float64).reshape(shp))
+            off += 8 * cnt
+        rec["cmask"].append(int(np.frombuffer(raw[off:off + 4], dtype=np.int32)[0])); off += 4
+        rec["tau"].append(np.frombuffer(raw[off:off + 8 * n], dtype=np.float64)); off += 8 * n
+        rec["x"].append(np.frombuffer(raw[off:off + 8 * (n + 3 * nc)], dtype=np.float64)); off += 8 * (n + 3 * nc)
+        rec["status"].append(int(np.frombuffer(raw[off:off + 4], dtype=np.int32)[0])); off += 4
+    assert off == len(raw)
+    out = {k: np.ascontiguousarray(np.array(v)) for k, v in rec.items()}
+    out["cmask"] = out["cmask"].astype(np.int32)
+    return n, nc, out
+
+
+def test_forceacc_dummy_driver_matches_oracle(tmp_path, oracle_lib):
+    """ForceAccExample (contact form, 4 feet, pelvis waist task) in dummy mode on the synthetic
+    floating-base quadruped: every dumped tick re-solved by the oracle's contact form."""
+    from qppvm_amd import build
+    from qppvm_amd.problem import ContactProblem
+    driver = build.build_plugins()[1]
+    dump = str(tmp_path / "dump_fa.bin")
+    r = subprocess.run([driver, "--plugin", "forceacc", "--ticks", "200", "--dump", dump, "40"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert '"plugin": "ForceAccExample"' in r.stdout
+    n, nc, d = read_forceacc_dump(dump)
+    prob = ContactProblem(n=n, nc=nc)
+    inp = {k: d[k] for k in ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref", "Jc", "jdqd_c",
+                             "pose_c", "pose_c_ref", "cmask")}
+    tau_r, x_r, st_r, _, _ = oracle_lib.contact_batch(prob, inp)
     np.testing.assert_array_equal(d["status"], st_r)
     ok = st_r == 0
     assert ok.sum() >= len(ok) - 2
