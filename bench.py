@@ -5,7 +5,9 @@ already resident in HBM. Default workload = BASELINE config 1 (4096 identical QP
 instances per GPU); ``--form contact`` runs the contact-form (ForceAcc) variant, and the
 default run also measures that variant for a few hundred steps and reports it beside
 the headline line. ``--config 2`` = random states (QPPVM: ~20 % of torque bounds active;
-contact: 2/3/4 of 4 feet in contact + actuated torque rows).
+contact: 2/3/4 of 4 feet in contact + actuated torque rows); ``--config 4`` = MPC: a step is
+one rollout of N = 20 sequential solves per instance with q, qd integrated on the device
+(wbq_rollout), counted as B x 20 QPs.
 
 N > 1: one process per GPU (torch.distributed.run), each rank solves its own shard of B
 instances (weak scaling, no data-path collective unless --allgather). Prints ONE JSON line
@@ -38,6 +40,7 @@ METRIC = "batched WBC-QP solves/sec, ~30-DoF problem, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 DOMINANT = {"qppvm": "qppvm_fast_kernel", "contact": "contact_kernel"}
 TIMING_EVERY = 8  # HIP-event pairs around every 8th solve of the timed region
+HORIZON, MPC_DT = 20, 1e-3  # config 4: N = 20 sequential QPs per rollout, semi-implicit Euler
 
 
 def qppvm_bytes(n, T):
@@ -61,6 +64,8 @@ def build_workload(form, config, n, B, world, rank, device):
     from qppvm_amd.synth import contact_instances, qppvm_instances, replicate
     from qppvm_amd.wbq import ContactSolver, QPPVMSolver
     plan = ShardPlan(B * world, world)  # weak scaling: rank r solves rows [r B, (r+1) B)
+    if config == 4:
+        config = 2  # MPC rollouts start from the config-2 random states
     if form == "qppvm":
         if config == 1:
             prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive
@@ -102,8 +107,17 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         solver.set_stream(torch.cuda.current_stream().cuda_stream)
         solver.set_device_outputs(out.data_ptr())
 
+    if config == 4:  # each MPC step re-plans from the measured state: a D2D reset of (q, qd)
+        q0 = torch.from_numpy(np.ascontiguousarray(inp["q"])).to(f"cuda:{device}")
+        qd0 = torch.from_numpy(np.ascontiguousarray(inp["qd"])).to(f"cuda:{device}")
+        torch.cuda.synchronize()
+
     def step():
-        solver.solve()
+        if config == 4:
+            solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
+            solver.rollout(HORIZON, MPC_DT)
+        else:
+            solver.solve()
         if gather_buf is not None:
             if dist:
                 import torch.distributed as tdist
@@ -138,8 +152,9 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt, kavg_ms, savg_ms = float(t[0]), float(t[1]), float(t[2])
     per_inst = qppvm_bytes(n, prob.ntasks) if form == "qppvm" else contact_bytes(n, prob.nc)
+    qps = HORIZON if config == 4 else 1  # an MPC step counts its N sequential QPs
     return dict(prob=prob, inp=inp, dt=dt, t_enq=t_enq, kavg_ms=kavg_ms, savg_ms=savg_ms, status=status, iters=iters,
-                bytes_per_instance=per_inst, total=B * world * steps)
+                bytes_per_instance=per_inst, total=B * world * steps * qps)
 
 
 def pmc_traffic(args, form):
@@ -204,8 +219,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
     ap.add_argument("--n", type=int, default=30)
     ap.add_argument("--form", choices=("qppvm", "contact"), default="qppvm")
-    ap.add_argument("--config", type=int, default=1, choices=(1, 2),
-                    help="1: identical instances; 2: random states, bounds / contacts churn")
+    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 4),
+                    help="1: identical instances; 2: random states, bounds / contacts churn; "
+                         "4: MPC, each step = HORIZON sequential solves per rollout (wbq_rollout)")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -234,7 +250,10 @@ def main():
     wl = {("qppvm", 1): "QPPVM 2-level torque QP, identical instances, bounds inactive (BASELINE config 1)",
           ("qppvm", 2): "QPPVM 2-level torque QP, random states, ~20% torque bounds active (config 2)",
           ("contact", 1): "ForceAcc contact-form QP, double support (nc=2), identical instances (config 1 variant)",
-          ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows (config 2)"}
+          ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows (config 2)",
+          ("qppvm", 4): f"MPC: rollouts x N={HORIZON} sequential QPPVM QPs, on-device semi-implicit Euler "
+                        "(dt=1e-3), J/M/h frozen, warm-start carry (config 4)",
+          ("contact", 4): f"MPC: rollouts x N={HORIZON} sequential contact-form QPs, on-device Euler (config 4)"}
     line = {
         "metric": METRIC,
         "value": value,

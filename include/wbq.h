@@ -22,6 +22,8 @@
  *                        bool of solve() (:246) as a per-instance status.
  *   wbq_reset_warmstart <- qpOASES hot-start state reset (QPOases_sot re-init) [upstream].
  *   wbq_destroy       <- plugin close()/destructor (:339-342).
+ *   wbq_rollout       <- no reference counterpart: the MPC config, N
+ *                        solves with the state integrated on the device between them.
  *
  * Contact form (ForceAcc plugin, src/ForceAcc.cpp):
  *   wbq_create_contact      <- ForceAccExample::init_control_plugin's wiring (:31-141: OptvarHelper
@@ -142,6 +144,19 @@ int wbq_set_stream(wbq_ctx *ctx, void *hip_stream);
 int wbq_set_inputs(wbq_ctx *ctx, const wbq_inputs *in);
 int wbq_set_contact_inputs(wbq_ctx *ctx, const wbq_contact_inputs *in);
 int wbq_solve(wbq_ctx *ctx);
+/* MPC-style rollout: `steps` sequential solves of the current batch,
+ * each followed on the device by qdd = M^-1 (tau - h) (the contact form: x[0:n]) and
+ * semi-implicit Euler qd += dt qdd, q += dt qd on the batch's q and qd in place (J, M, h and
+ * poses frozen; mirrors the integration ForceAcc.cpp:225-226 leaves commented out). The
+ * per-instance warm-start state carries from step to step. Host-staged inputs advance in the
+ * context's copy, WBQ_MEM_DEVICE inputs in the caller's buffers. Outputs afterwards are the
+ * last step's. */
+int wbq_rollout(wbq_ctx *ctx, int steps, double dt);
+/* Synchronous copy of the batch's current q, qd ([batch][n], either may be NULL). */
+int wbq_get_state(wbq_ctx *ctx, double *q, double *qd);
+/* Overwrite the batch's q, qd ([batch][n], either may be NULL; WBQ_MEM_*), stream-ordered: the
+ * start state of the next rollout (an MPC re-plans each horizon from the measured state). */
+int wbq_set_state(wbq_ctx *ctx, const double *q, const double *qd, int memory);
 int wbq_sync(wbq_ctx *ctx);
 /* Synchronous copy of the last solve's outputs to host memory (any pointer may be NULL). */
 int wbq_get_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);

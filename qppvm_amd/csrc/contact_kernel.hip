@@ -752,6 +752,7 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     if (ok && tmax > 0.0) status = 3;
     if (status != 0) tau_i = h_i;
     if (qrow) a.tau[b * n + i] = tau_i;
+    rollout_step(a, b, i, qrow, S[L.XV + i], status == 0); // qdd = x[0:n]
     if (i < L.NX) a.x[b * L.NX + i] = status == 0 ? S[L.XV + i] : 0.0;
     if (i == 0) {
         a.status[b] = status;

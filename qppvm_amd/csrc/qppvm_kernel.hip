@@ -806,6 +806,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
             if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
             if (row) a.tau[b * n + i] = tau_i;
+            rollout_step(a, b, i, row, S[L.U + i], status == 0); // qdd = M^-1 x = u
             if (valid && i == 0) {
                 a.status[b] = status;
                 a.iters[b] = iters;
@@ -856,6 +857,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
         if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
         if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
         if (row) a.tau[b * n + i] = tau_i;
+        rollout_step(a, b, i, row, S[L.U + i], status == 0);
         if (valid && i == 0) {
             a.status[b] = status;
             a.iters[b] = iters + ro.it;
@@ -1106,6 +1108,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         double tau_i = x_i + h_i;
         if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
         if (row) a.tau[bn + i] = tau_i;
+        rollout_step(a, b, i, row, u_i, status == 0); // qdd = M^-1 (tau - h) = u
         if (valid && i == 0) {
             a.status[b] = status;
             a.iters[b] = 0;
@@ -1143,6 +1146,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
                     if (!isfinite(tau2) && st2 == 0) st2 = 3;
                     if (st2 != 0) tau2 = h_i;
                     if (row) a.tau[bn + i] = tau2;
+                    rollout_step(a, b, i, row, S[LA.U + i], st2 == 0);
                     if (i == 0) {
                         a.status[b] = st2;
                         a.iters[b] = it2;
@@ -1179,7 +1183,10 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
     return hipGetLastError();
 }
 
-constexpr unsigned kFollowGrid = 512; // 2 blocks per CU
+// Follow-up grid cap: 2 waves per SIMD over the whole chip (launch cost measured independent of
+// the grid size, scripts/launch_probe.hip; a smaller cap starves a solve where many instances
+// need the repair, e.g. diverging MPC rollouts)
+constexpr unsigned kFollowGrid = 2048;
 
 template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)

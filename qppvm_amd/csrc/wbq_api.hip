@@ -120,7 +120,7 @@ int hip_fail(wbq_ctx *c, hipError_t e, const char *what)
         if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
     } while (0)
 
-int solve_contact(wbq_ctx *c)
+int solve_contact(wbq_ctx *c, int integrate, double dt)
 {
     const wbq_contact_desc &d = c->cd;
     wbq::ContactArgs a{};
@@ -162,6 +162,8 @@ int solve_contact(wbq_ctx *c)
     a.iters = c->out_iters ? c->out_iters : c->iters;
     a.x = c->dev_x;
     a.stamps = c->stamps;
+    a.integrate = integrate;
+    a.dt = dt;
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
                        (c->solves++ % (unsigned long long)c->timing_every) == 0;
@@ -430,11 +432,11 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
     return WBQ_SUCCESS;
 }
 
-int wbq_solve(wbq_ctx *c)
+static int solve_impl(wbq_ctx *c, int integrate, double dt)
 {
     if (!c) return WBQ_E_INVALID;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "wbq_set_inputs not called");
-    if (c->form == WBQ_FORM_CONTACT) return solve_contact(c);
+    if (c->form == WBQ_FORM_CONTACT) return solve_contact(c, integrate, dt);
     wbq::QppvmArgs a{};
     a.B = c->batch;
     a.n = c->d.n;
@@ -472,6 +474,8 @@ int wbq_solve(wbq_ctx *c)
     a.epoch = c->epoch;
     a.ws_hint = c->ws_hint;
     a.ws_state = c->ws_state;
+    a.integrate = integrate;
+    a.dt = dt;
 
     WBQ_HIP(hipSetDevice(c->device));
     // timed solves record (start, after the dominant first kernel, end) on the launch stream
@@ -487,6 +491,51 @@ int wbq_solve(wbq_ctx *c)
         c->ev_mid[c->ev_used / 3] = single ? 2 : 1;
         c->ev_used += 3;
     }
+    return WBQ_SUCCESS;
+}
+
+int wbq_solve(wbq_ctx *c) { return solve_impl(c, 0, 0.0); }
+
+int wbq_rollout(wbq_ctx *c, int steps, double dt)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout: steps >= 0, dt >= 0");
+    for (int k = 0; k < steps; ++k) {
+        const int rc = solve_impl(c, 1, dt);
+        if (rc != WBQ_SUCCESS) return rc;
+    }
+    return WBQ_SUCCESS;
+}
+
+int wbq_get_state(wbq_ctx *c, double *q, double *qd)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
+    if (c->batch == 0) return WBQ_SUCCESS;
+    WBQ_HIP(hipSetDevice(c->device));
+    const size_t bytes = (size_t)c->batch * c->d.n * 8;
+    const double *dq = c->form == WBQ_FORM_CONTACT ? c->in[2] : c->in[4];
+    const double *dqd = c->form == WBQ_FORM_CONTACT ? c->in[3] : c->in[5];
+    if (q) WBQ_HIP(hipMemcpyAsync(q, dq, bytes, hipMemcpyDeviceToHost, c->stream));
+    if (qd) WBQ_HIP(hipMemcpyAsync(qd, dqd, bytes, hipMemcpyDeviceToHost, c->stream));
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    return WBQ_SUCCESS;
+}
+
+int wbq_set_state(wbq_ctx *c, const double *q, const double *qd, int memory)
+{
+    if (!c) return WBQ_E_INVALID;
+    if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
+    if (memory != WBQ_MEM_DEVICE && memory != WBQ_MEM_HOST) return fail(c, WBQ_E_INVALID, "unknown memory kind");
+    if (c->batch == 0) return WBQ_SUCCESS;
+    WBQ_HIP(hipSetDevice(c->device));
+    const size_t bytes = (size_t)c->batch * c->d.n * 8;
+    double *dq = const_cast<double *>(c->form == WBQ_FORM_CONTACT ? c->in[2] : c->in[4]);
+    double *dqd = const_cast<double *>(c->form == WBQ_FORM_CONTACT ? c->in[3] : c->in[5]);
+    const hipMemcpyKind kind = memory == WBQ_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (q) WBQ_HIP(hipMemcpyAsync(dq, q, bytes, kind, c->stream));
+    if (qd) WBQ_HIP(hipMemcpyAsync(dqd, qd, bytes, kind, c->stream));
+    if (memory == WBQ_MEM_HOST) WBQ_HIP(hipStreamSynchronize(c->stream)); // caller may reuse its buffers
     return WBQ_SUCCESS;
 }
 

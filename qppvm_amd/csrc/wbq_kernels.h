@@ -46,6 +46,10 @@ struct QppvmArgs {
     // directly; state = BVLS bound state (-1/0/+1 per joint) of that repair
     unsigned char *ws_hint; // [B]
     signed char *ws_state;  // [B][NP]
+    // MPC rollout step (wbq_rollout): after the final tau of an instance, qdd = M^-1 (tau - h)
+    // and semi-implicit Euler on q, qd in place
+    int integrate;
+    double dt;
 };
 
 constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
@@ -81,7 +85,22 @@ struct ContactArgs {
     int *status;     // [B]
     int *iters;      // [B]
     unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [B][kStamps] s_memtime
+    int integrate;   // MPC rollout step: qdd = x[0:n], semi-implicit Euler on q, qd in place
+    double dt;
 };
+
+// Semi-implicit Euler of one joint of instance b in place (lane i owns joint i of its
+// instance): qd += dt qdd, q += dt qd. Failed solves (tau = h) have qdd = M^-1 (tau - h) = 0.
+template <typename Args>
+__device__ __forceinline__ void rollout_step(const Args &a, long b, int i, bool row, double qdd, bool ok)
+{
+    if (!a.integrate || !row) return;
+    double *q = const_cast<double *>(a.q), *qd = const_cast<double *>(a.qd);
+    const long k = b * a.n + i;
+    const double v = qd[k] + a.dt * (ok ? qdd : 0.0);
+    qd[k] = v;
+    q[k] = q[k] + a.dt * v;
+}
 
 hipError_t launch_contact(const ContactArgs &a, hipStream_t stream);
 

@@ -24,7 +24,8 @@ FORM_QPPVM, FORM_CONTACT = 0, 1
 EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
            "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
-           "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail")
+           "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail", "wbq_rollout",
+           "wbq_get_state", "wbq_set_state")
 
 
 class WbqError(RuntimeError):
@@ -94,10 +95,14 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_create_contact.argtypes = [ctypes.POINTER(ContactDesc), I, ctypes.POINTER(P)]
     lib.wbq_set_contact_inputs.argtypes = [P, ctypes.POINTER(ContactInputs)]
     lib.wbq_get_contact_outputs.argtypes = [P, P]
+    lib.wbq_rollout.argtypes = [P, I, ctypes.c_double]
+    lib.wbq_get_state.argtypes = [P, P, P]
+    lib.wbq_set_state.argtypes = [P, P, P, I]
     for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
               "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
               "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
-              "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail"):
+              "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail",
+              "wbq_rollout", "wbq_get_state", "wbq_set_state"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib
@@ -196,6 +201,27 @@ class QPPVMSolver:
         self._check(self.lib.wbq_get_device_outputs(self.ctx, ctypes.byref(t), ctypes.byref(s),
                                                     ctypes.byref(i)), "wbq_get_device_outputs")
         return t.value, s.value, i.value
+
+    def rollout(self, steps: int, dt: float = 1e-3):
+        """``steps`` solves with q, qd integrated on the device between them (wbq_rollout)."""
+        self._check(self.lib.wbq_rollout(self.ctx, int(steps), float(dt)), "wbq_rollout")
+
+    def state(self):
+        """The batch's current (q, qd) on the device."""
+        q = np.empty((self.batch, self.prob.n))
+        qd = np.empty((self.batch, self.prob.n))
+        self._check(self.lib.wbq_get_state(self.ctx, _ptr(q), _ptr(qd)), "wbq_get_state")
+        return q, qd
+
+    def set_state(self, q=None, qd=None, device: bool = False):
+        """Overwrite (q, qd): numpy arrays, or device pointers (ints) with device=True."""
+        if device:
+            self._check(self.lib.wbq_set_state(self.ctx, q or None, qd or None, MEM_DEVICE), "wbq_set_state")
+            return
+        qa = None if q is None else np.ascontiguousarray(q, dtype=np.float64)
+        qda = None if qd is None else np.ascontiguousarray(qd, dtype=np.float64)
+        self._check(self.lib.wbq_set_state(self.ctx, None if qa is None else _ptr(qa),
+                                           None if qda is None else _ptr(qda), MEM_HOST), "wbq_set_state")
 
     def solve_batch(self, inputs: dict):
         self.set_inputs(inputs)

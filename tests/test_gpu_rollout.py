@@ -1,0 +1,111 @@
+"""GPU: MPC-style rollouts through wbq_rollout. Each step solves the
+batch, then q_dd = M^-1 (tau - h) (contact form: x[0:n]) and semi-implicit Euler
+qd += dt q_dd, q += dt qd on the device; J, M, h and poses are frozen per rollout. The CPU
+check runs the same loop with the oracle and numpy: the torques of the last step within the
+1e-6 relative tolerance, the states to 1e-9 relative."""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from qppvm_amd.problem import ContactProblem, QPPVMProblem
+from qppvm_amd.synth import contact_instances, qppvm_instances
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def wbq_mod():
+    from qppvm_amd import build, wbq
+    build.build()
+    return wbq
+
+
+def cpu_rollout_qppvm(oracle_lib, prob, inp, steps, dt):
+    inp = {k: v.copy() for k, v in inp.items()}
+    for _ in range(steps):
+        tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
+        qdd = np.linalg.solve(inp["M"], (tau - inp["h"])[..., None])[..., 0]
+        qdd[st != 0] = 0.0
+        inp["qd"] = inp["qd"] + dt * qdd
+        inp["q"] = inp["q"] + dt * inp["qd"]
+    return tau, st, inp["q"], inp["qd"]
+
+
+@pytest.mark.parametrize("n,tau_max", [(30, 1e6), (30, None), (39, None)])
+def test_rollout_qppvm_matches_cpu_loop(wbq_mod, oracle_lib, n, tau_max):
+    base = QPPVMProblem(n=n)
+    inp = qppvm_instances(base, 48, seed=90 + n)
+    if tau_max is None:  # ~20 % of the torque limits binding along the rollout
+        free = QPPVMProblem(n=n, tau_max=1e9)
+        tau0, _, _ = oracle_lib.qppvm_batch(free, inp)
+        tau_max = float(np.quantile(np.abs(tau0), 0.8))
+    prob = QPPVMProblem(n=n, tau_max=tau_max)
+    steps, dt = 6, 1e-3
+    tau_r, st_r, q_r, qd_r = cpu_rollout_qppvm(oracle_lib, prob, inp, steps, dt)
+    s = wbq_mod.QPPVMSolver(prob, max_batch=48)
+    s.set_inputs(inp)
+    s.rollout(steps, dt)
+    tau, st, _ = s.outputs()
+    q, qd = s.state()
+    s.close()
+    np.testing.assert_array_equal(st, st_r)
+    ok = st == 0
+    assert rel_err(tau[ok], tau_r[ok]) <= TOL
+    assert rel_err(qd, qd_r) <= 1e-9 and rel_err(q, q_r) <= 1e-9
+    assert np.abs(qd - inp["qd"]).max() > 0.0  # the state did move
+
+
+def test_rollout_contact_matches_cpu_loop(wbq_mod, oracle_lib):
+    prob = ContactProblem(n=30, nc=4)
+    inp = contact_instances(prob, 32, seed=77, masks=[0b0011, 0b0111, 0b1111])
+    steps, dt = 5, 1e-3
+    ref = {k: v.copy() for k, v in inp.items()}
+    for _ in range(steps):
+        tau_r, x_r, st_r, _, _ = oracle_lib.contact_batch(prob, ref)
+        qdd = np.where((st_r == 0)[:, None], x_r[:, :30], 0.0)
+        ref["qd"] = ref["qd"] + dt * qdd
+        ref["q"] = ref["q"] + dt * ref["qd"]
+    s = wbq_mod.ContactSolver(prob, max_batch=32)
+    s.set_inputs(inp)
+    s.rollout(steps, dt)
+    tau, st, _ = s.outputs()
+    q, qd = s.state()
+    s.close()
+    np.testing.assert_array_equal(st, st_r)
+    assert rel_err(tau[st == 0], tau_r[st_r == 0]) <= TOL
+    assert rel_err(qd, ref["qd"]) <= 1e-9 and rel_err(q, ref["q"]) <= 1e-9
+
+
+def test_rollout_zero_steps_and_plain_solve_leave_state(wbq_mod):
+    prob = QPPVMProblem(n=30, tau_max=1e6)
+    inp = qppvm_instances(prob, 8, seed=3)
+    s = wbq_mod.QPPVMSolver(prob, max_batch=8)
+    s.set_inputs(inp)
+    s.rollout(0)
+    s.solve()
+    q, qd = s.state()
+    s.close()
+    np.testing.assert_array_equal(q, inp["q"])
+    np.testing.assert_array_equal(qd, inp["qd"])
+
+
+def test_set_state_restarts_rollout(wbq_mod):
+    """wbq_set_state: two rollouts from the same start state agree (the second starts warm: the
+    warm start changes the path, not the solution, so agreement is to roundoff)."""
+    prob = QPPVMProblem(n=30, tau_max=60.0)
+    inp = qppvm_instances(prob, 16, seed=5)
+    s = wbq_mod.QPPVMSolver(prob, max_batch=16)
+    s.set_inputs(inp)
+    s.rollout(4, 1e-3)
+    q1, qd1 = s.state()
+    tau1, _, _ = s.outputs()
+    s.set_state(inp["q"], inp["qd"])
+    q0, qd0 = s.state()
+    np.testing.assert_array_equal(q0, inp["q"])
+    s.rollout(4, 1e-3)
+    q2, qd2 = s.state()
+    tau2, _, _ = s.outputs()
+    s.close()
+    assert rel_err(q1, q2) <= 1e-12 and rel_err(qd1, qd2) <= 1e-12
+    assert rel_err(tau1, tau2) <= 1e-9
