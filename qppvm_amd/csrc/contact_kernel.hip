@@ -36,6 +36,8 @@
 #include "wbq_kernels.h"
 #include "wbq_device.h"
 
+#include <type_traits>
+
 namespace wbq {
 namespace {
 
@@ -47,7 +49,7 @@ namespace {
 // X = H^-1 A_q^T has one column ("slot") per q-bearing row, slot = ci, plus x0 at NJ + 6.
 struct ContactLayout {
     int NJ, NR, ME, NX, QS, FS, GS, TS;
-    int AQJ, AQW, FFJ, XT, GM, TT, TC, GA, JC, PN, RH, HR, XV, X0, VV, LV, RV, WV, DUM, AC, PS, BT, JD, QD, SIZE;
+    int AQJ, AQW, FFJ, XT, GM, TT, JC, PN, RH, HR, XV, X0, VV, LV, RV, WV, DUM, AC, PS, BT, JD, QD, SIZE;
     __host__ __device__ ContactLayout(int n, int nc, bool tr, int NQ, int NRC)
     {
         NJ = tr ? n : 6;
@@ -71,9 +73,7 @@ struct ContactLayout {
         RH = TT + ov; ov += 2 * 4 * NRC;      // its right-hand sides
         HR = TT + ov; ov += (NQ == 64 && tr) ? NQ * QS : 0; // H rows for a second rhs chunk
         // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns
-        const int tt = tr ? (2 * NX + ME) * TS : 12 * TS; // (!tr: scratch for the T_E rows)
-        TC = TT + NX * TS;
-        GA = TC + NX * TS;
+        const int tt = tr ? NX * TS : 12 * TS; // (!tr: scratch for the T_E rows)
         o += tt > ov ? tt : ov;
         XV = o; o += 64;          // x
         X0 = o; o += 64;          // x0 = -H^-1 g
@@ -82,7 +82,7 @@ struct ContactLayout {
         RV = o; o += 72;
         WV = o; o += 72;
         DUM = o; o += 72;         // row of the lanes that own no slot-vector row
-        AC = o; o += 64;          // active constraint (compact index) per slot
+        AC = o; o += 72;          // active constraint (compact index) per slot (+8: chunked gathers)
         PS = o; o += 24 * (1 + kCMax);   // poses: waist, then contacts ([R|p], ref)
         BT = o; o += 6 * (1 + kCMax);    // task targets: waist b_w, then b_c
         JD = o; o += 6 * (1 + kCMax);    // Jdot qd
@@ -248,6 +248,68 @@ __device__ __forceinline__ double bcast(double v, int lane)
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
+
+// LDS views for the torque-rows variant, with no storage of their own: column a of T read
+// from the T rows (lane a: T[c][a] = TT[c TS + a]), and Gamma[j][act_q] gathered through the
+// slot list AC; chunks of 8 independent loads. Their writes are no-ops (the data is in TT, GM).
+struct TColView {
+    const double *tt;
+    int ts;
+    __device__ void bind(const double *col, int stride)
+    {
+        tt = col;
+        ts = stride;
+    }
+    __device__ void zero_from(int) {}
+    __device__ void put(int, bool, double) {}
+    __device__ void put_dyn(int, bool, double) {}
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int c0 = 0; c0 < cnt; c0 += 8) {
+            double pv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                pv[u] = tt[(c0 + u) * ts];
+                bv[u] = b[c0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+        }
+        return s;
+    }
+};
+
+struct GAView {
+    const double *grow, *ac;
+    __device__ void bind(const double *row, const double *slots)
+    {
+        grow = row;
+        ac = slots;
+    }
+    __device__ void zero_from(int) {}
+    __device__ void put(int, bool, double) {}
+    __device__ void put_dyn(int, bool, double) {}
+    __device__ void shift_down(int, int) {}
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int q0 = 0; q0 < cnt; q0 += 8) {
+            int cq[8];
+            double bv[8], gv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cq[u] = q0 + u < cnt ? (int)ac[q0 + u] : 0;
+                bv[u] = b[q0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) gv[u] = grow[cq[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(q0 + u < cnt ? gv[u] : 0.0, q0 + u < cnt ? bv[u] : 0.0, s);
+        }
+        return s;
+    }
+};
 
 // compact index of equality a (a < 6: dynamic feasibility rows, then the waist rows)
 __device__ __forceinline__ int eq_row(int a, int NJ) { return a < 6 ? a : NJ + a - 6; }
@@ -469,11 +531,15 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     // activity s_j and GA_j[q] = Gamma[j][act_q].
     constexpr bool SREG = !TR;      // without torque rows k <= 12 + 3 nc <= KMR: registers
     constexpr int KM = TR ? 64 : KMR;
-    SlotVec<KM, SREG> Trow, Tcol, GA;
+    using TcolT = typename std::conditional<SREG, SlotVec<KM, true>, TColView>::type;
+    using GAT = typename std::conditional<SREG, SlotVec<KM, true>, GAView>::type;
+    SlotVec<KM, SREG> Trow;
+    TcolT Tcol;
+    GAT GA;
     if constexpr (!SREG) {
         Trow.bind(S + (i < L.NX ? L.TT + i * L.TS : L.DUM), L.NX);
-        Tcol.bind(S + (i < L.NX ? L.TC + i * L.TS : L.DUM), L.NX);
-        GA.bind(S + (ci < ME ? L.GA + ci * L.TS : L.DUM), L.NX);
+        Tcol.bind(S + L.TT + (i < L.NX ? i : 0), L.TS);
+        GA.bind(S + L.GM + (ci < ME ? ci : 0) * L.GS, S + L.AC);
     }
     Trow.zero_from(0);
     Tcol.zero_from(0);
@@ -530,6 +596,7 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         }
         const double ye = __shfl(lo - s_i, er); // e_E - s_E (every lane active: sources up to lane NJ + 5)
         if (i < 12) S[L.VV + i] = ye;
+        S[L.AC + i] = (double)er; // slots 0..11 (the gathered Gamma columns of the LDS variant)
         __syncthreads();
         if constexpr (SREG) Trow.load_if(i < 12, S + L.TT + (i < 12 ? i : 0) * L.TS, 12);
         const double w = i < 12 ? Trow.dot(S + L.VV, 12) : 0.0;
@@ -635,6 +702,7 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
         const double gpp = S[L.GM + cp * L.GS + cp];
         S[L.VV + i] = i < k ? sgn * sgp * S[L.GM + act * L.GS + cp] : 0.0;
+        S[L.AC + i] = (double)act;
         __syncthreads();
         const double l = i < k ? Trow.dot(S + L.VV, k) : 0.0;
         S[L.LV + i] = l;
