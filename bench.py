@@ -92,7 +92,7 @@ def build_workload(form, config, n, B, world, rank, device):
     return prob, inp, ContactSolver
 
 
-def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False):
+def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False):
     """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
     import torch
     prob, inp, Solver = build_workload(form, config, n, B, world, rank, device)
@@ -113,6 +113,11 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         torch.cuda.synchronize()
 
     def step():
+        if host_io:  # PCIe-inclusive: host inputs -> pinned staging -> H2D, solve, D2H outputs
+            solver.set_inputs(inp)
+            solver.solve()
+            solver.outputs()
+            return
         if config == 4:
             solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
             solver.rollout(HORIZON, MPC_DT)
@@ -211,6 +216,30 @@ def cpu_baseline(form, prob, inp, budget_s):
             "sample": f"{done} instances of the bench batch in {dt:.1f} s, oracle ({what}), 1 thread"}
 
 
+def cpu_baseline_threads(form, prob, inp, budget_s):
+    """Same oracle, one independent instance stream per host thread (the
+    all-cores run); the C calls release the GIL. Threads = the box's CPU share (16)."""
+    import concurrent.futures as cf
+    import oracle
+    fn = oracle.qppvm_batch if form == "qppvm" else oracle.contact_batch
+    T = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    B = inp["h"].shape[0]
+
+    def worker(w):
+        done, t0, chunk = 0, time.perf_counter(), 32
+        while time.perf_counter() - t0 < budget_s:
+            lo = (w * 257 + done) % B
+            fn(prob, {k: v[lo:lo + chunk] for k, v in inp.items()})
+            done += min(chunk, B - lo)
+        return done
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=T) as ex:
+        done = sum(ex.map(worker, range(T)))
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "QP-solves/s", "cores": T, "kind": "port",
+            "sample": f"{done} instances in {dt:.1f} s, {T} threads, one instance stream each"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +256,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     ap.add_argument("--no-variant", action="store_true", help="skip the contact-form variant line")
+    ap.add_argument("--host-io", action="store_true",
+                    help="PCIe-inclusive rate: host inputs copied in and outputs copied out every step "
+                         "(never the headline value; DESIGN.md reports it beside it)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -243,7 +275,8 @@ def main():
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = local if dist else 0
     n, B = args.n, args.batch
-    m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, args.allgather, dist)
+    m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, args.allgather, dist,
+            args.host_io)
     value = m["total"] / m["dt"]
     bpl = m["bytes_per_instance"] * B
     achieved = bpl / (m["kavg_ms"] * 1e-3) / 1e9
@@ -266,7 +299,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic randomized robot states (SURVEY 8d), inputs resident in HBM",
+        "data": "synthetic randomized robot states (SURVEY 8d), " + (
+            "host inputs/outputs over PCIe every step (--host-io)" if args.host_io else "inputs resident in HBM"),
         "config": {"workload": f"{wl[(args.form, args.config)]}, n={n}, batch={B}/GPU",
                    "global_batch": B * world, "n": n, "parallelism": f"shard{world}",
                    "allgather": bool(args.allgather)},
@@ -295,6 +329,7 @@ def main():
                                    "mean_active_set_steps": float(np.mean(v["iters"]))}
     if rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.form, m["prob"], m["inp"], args.cpu_seconds)
+        line["cpu_baseline_threads"] = cpu_baseline_threads(args.form, m["prob"], m["inp"], args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
