@@ -29,7 +29,7 @@ def run(libpath, prob, inp, reps=20, stamps=False):
     out = {"us_per_launch": 1e3 * ms / cnt}
     if stamps:
         B = inp["h"].shape[0]
-        nb = (B + 1) // 2 if prob.n <= 32 else B
+        nb = B if (prob.n > 32 or os.environ.get("WBQ_MFMA_MAX_BATCH", "1") != "0") else (B + 1) // 2
         K = 16
         buf = (ctypes.c_ulonglong * (K * nb))()
         s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -40,7 +40,7 @@ def run(libpath, prob, inp, reps=20, stamps=False):
         out["fast_kernel_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in enumerate(PHASES)}
         out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
         _, status, iters = s.outputs()
-        it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if prob.n <= 32 else iters[:nb]
+        it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if nb < B else iters[:nb]
         act = it_blk > 0
         if act.any():
             setup = full[act, 6] - full[act, 4]
@@ -64,8 +64,10 @@ def run(libpath, prob, inp, reps=20, stamps=False):
 
 
 def main():
-    from qppvm_amd import build
-    diag = build.build(force=True, diag=True)
+    diag = os.path.join(ROOT, "qppvm_amd", "libwbq_diag.so")  # built beforehand, in-tree
+    if not os.path.exists(diag):
+        from qppvm_amd import build
+        diag = build.build(force=True, diag=True)
     res = {}
     n = 30
     base = qppvm_instances(QPPVMProblem(n=n), 65536, seed=1)
