@@ -896,13 +896,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const int voff = (int)(8 * (bn + ic));
     const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
     const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
-    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-    const int moff = (int)(8 * ((valid ? b * n * n : 0) + ic));
-    // M is symmetric: lane i's row is its column, so row r of M read across lanes is
-    // contiguous -- coalesced loads straight into the elimination registers.
-    double A[NP];
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    // J and the poses first, M last: vmcnt waits are in order, so the task forces (J, poses,
+    // qd) can start while M is still streaming in
     double jv[kTMax * 6];
     {
         const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.J, Bn * T * 6);
@@ -912,14 +907,28 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     }
     constexpr int kPoseIt = (kTMax * 24 + NP - 1) / NP;
     double pv[kPoseIt];
-#pragma unroll
-    for (int it = 0; it < kPoseIt; ++it) {
-        int e = it * NP + i;
-        e = e < T * 24 ? e : T * 24 - 1;
-        const int t = e / 24, c = e - t * 24;
+    {
         const long base = valid ? b * T * 12 : 0;
-        pv[it] = (c < 12) ? a.pose[base + t * 12 + c] : a.pose_ref[base + t * 12 + c - 12];
+        const __amdgpu_buffer_rsrc_t Prs = rsrc(a.pose, (long)a.B * T * 12);
+        const __amdgpu_buffer_rsrc_t Rrs = rsrc(a.pose_ref, (long)a.B * T * 12);
+#pragma unroll
+        for (int it = 0; it < kPoseIt; ++it) {
+            int e = it * NP + i;
+            e = e < T * 24 ? e : T * 24 - 1;
+            const int t = e / 24, c = e - t * 24;
+            const int cc = c < 12 ? c : c - 12;
+            const double p0 = bload(Prs, (int)(8 * (base + t * 12 + cc)), 0);
+            const double p1 = bload(Rrs, (int)(8 * (base + t * 12 + cc)), 0);
+            pv[it] = (c < 12) ? p0 : p1;
+        }
     }
+    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
+    const int moff = (int)(8 * ((valid ? b * n * n : 0) + ic));
+    // M is symmetric: lane i's row is its column, so row r of M read across lanes is
+    // contiguous -- coalesced loads straight into the elimination registers.
+    double A[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && a.ws_hint[b] != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
@@ -929,8 +938,6 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 #pragma unroll
     for (int it = 0; it < kPoseIt; ++it)
         if (it * NP + i < T * 24) S[L.PS + it * NP + i] = valid ? pv[it] : 0.0;
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     __syncthreads();
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
@@ -943,6 +950,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
         S[L.F + i] = F;
     }
+    // M (still streaming in during the forces): padding rows/columns past n -> identity
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
     // never has to be read again (a re-read of M would double the HBM bytes of the solve)
     double Y[M0];
