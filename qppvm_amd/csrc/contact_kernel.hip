@@ -35,6 +35,7 @@
 // point), 3 numerical. On status != 0: tau = h, x = 0.
 #include "wbq_kernels.h"
 #include "wbq_device.h"
+#include "dual_gi.h"
 
 #include <type_traits>
 
@@ -136,178 +137,39 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
     return xv[n + ci - L.NJ - 6];
 }
 
-// Per-lane vector of active-slot values (T rows, T columns, Gamma columns of the active
-// set): in registers (KM static; dynamic writes by select) or one LDS row per lane, whose
-// dots load in chunks of 8 independent reads. Either way the loads of a dot issue back to
-// back instead of one dependent LDS round trip per term.
-template <int KM, bool REG>
-struct SlotVec;
-
-template <int KM>
-struct SlotVec<KM, true> {
-    double v[KM];
-    __device__ void bind(double *, int) {}
-    __device__ void zero_from(int c)
+// The contact problem for dual_gi: Gamma in LDS, activities from the rows in LDS, and
+// x = x0 + H^-1 A^T w with H^-1 A_q^T from the X^T slots and the diagonal force block.
+template <int NQ>
+struct ContactGi {
+    double *S;
+    const ContactLayout *L;
+    int n, nf, i;
+    double ieps;
+    __device__ double gamma(int r, int c) const { return S[L->GM + r * L->GS + c]; }
+    __device__ double activity(int r) const { return wbq::activity<NQ>(S, *L, r, n, nf); }
+    __device__ void rebuild(int pass, int k) const
     {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) v[j] = (j >= c) ? 0.0 : v[j];
-    }
-    __device__ void zero_if(bool cond)
-    {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) v[j] = cond ? 0.0 : v[j];
-    }
-    __device__ void put(int c, bool cond, double x) { v[c] = cond ? x : v[c]; } // c static after unrolling
-    __device__ void put_dyn(int c, bool cond, double x)
-    {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) v[j] = (cond && j == c) ? x : v[j];
-    }
-    __device__ void load_if(bool cond, const double *src, int cnt)
-    {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            const double w = src[j];
-            v[j] = (cond && j < cnt) ? w : v[j];
-        }
-    }
-    __device__ void shift_down(int c, int cnt) // v[j] = v[j + 1] for c <= j < cnt - 1
-    {
-#pragma unroll
-        for (int j = 0; j + 1 < KM; ++j) v[j] = (j >= c && j + 1 < cnt) ? v[j + 1] : v[j];
-    }
-    __device__ double dot(const double *b, int cnt) const
-    {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            const double bj = b[j];
-            s = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s);
-        }
-        return s;
-    }
-};
-
-template <int KM>
-struct SlotVec<KM, false> {
-    double *p;
-    int cap;
-    __device__ void bind(double *row, int capacity)
-    {
-        p = row;
-        cap = capacity;
-    }
-    __device__ void zero_from(int c)
-    {
-        for (int j = c; j < cap; ++j) p[j] = 0.0;
-    }
-    __device__ void zero_if(bool cond)
-    {
-        if (cond)
-            for (int j = 0; j < cap; ++j) p[j] = 0.0;
-    }
-    __device__ void put(int c, bool cond, double x)
-    {
-        if (cond) p[c] = x;
-    }
-    __device__ void put_dyn(int c, bool cond, double x)
-    {
-        if (cond) p[c] = x;
-    }
-    __device__ void load_if(bool cond, const double *src, int cnt)
-    {
-        if (cond)
-            for (int j = 0; j < cnt; ++j) p[j] = src[j];
-    }
-    __device__ void shift_down(int c, int cnt)
-    {
-        for (int j = c; j + 1 < cnt; ++j) p[j] = p[j + 1];
-    }
-    __device__ double dot(const double *b, int cnt) const
-    {
-        double s = 0.0;
-        for (int c0 = 0; c0 < cnt; c0 += 8) {
-            double pv[8], bv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                pv[u] = p[c0 + u];
-                bv[u] = b[c0 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
-        }
-        return s;
-    }
-};
-
-// value of v in lane `lane` (uniform), as a scalar broadcast (v_readlane, no LDS)
-__device__ __forceinline__ double bcast(double v, int lane)
-{
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-// LDS views for the torque-rows variant, with no storage of their own: column a of T read
-// from the T rows (lane a: T[c][a] = TT[c TS + a]), and Gamma[j][act_q] gathered through the
-// slot list AC; chunks of 8 independent loads. Their writes are no-ops (the data is in TT, GM).
-struct TColView {
-    const double *tt;
-    int ts;
-    __device__ void bind(const double *col, int stride)
-    {
-        tt = col;
-        ts = stride;
-    }
-    __device__ void zero_from(int) {}
-    __device__ void put(int, bool, double) {}
-    __device__ void put_dyn(int, bool, double) {}
-    __device__ double dot(const double *b, int cnt) const
-    {
-        double s = 0.0;
-        for (int c0 = 0; c0 < cnt; c0 += 8) {
-            double pv[8], bv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                pv[u] = tt[(c0 + u) * ts];
-                bv[u] = b[c0 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
-        }
-        return s;
-    }
-};
-
-struct GAView {
-    const double *grow, *ac;
-    __device__ void bind(const double *row, const double *slots)
-    {
-        grow = row;
-        ac = slots;
-    }
-    __device__ void zero_from(int) {}
-    __device__ void put(int, bool, double) {}
-    __device__ void put_dyn(int, bool, double) {}
-    __device__ void shift_down(int, int) {}
-    __device__ double dot(const double *b, int cnt) const
-    {
-        double s = 0.0;
-        for (int q0 = 0; q0 < cnt; q0 += 8) {
+        if (i >= L->NX) return;
+        double dx = 0.0; // slots in chunks of 8 loads
+        const int fi = i - n;
+        for (int q0 = 0; q0 < k; q0 += 8) {
             int cq[8];
-            double bv[8], gv[8];
+            double wq[8], xq[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                cq[u] = q0 + u < cnt ? (int)ac[q0 + u] : 0;
-                bv[u] = b[q0 + u];
+                cq[u] = q0 + u < k ? (int)S[L->AC + q0 + u] : 0;
+                wq[u] = q0 + u < k ? S[L->RV + q0 + u] : 0.0;
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) gv[u] = grow[cq[u]];
+            for (int u = 0; u < 8; ++u) {
+                const int c = cq[u] < L->NJ + 6 ? cq[u] : 0;
+                xq[u] = i < n ? (cq[u] < L->NJ + 6 ? S[L->XT + c * L->QS + i] : 0.0) : fcoef(S, *L, cq[u], fi < 0 ? 0 : fi);
+            }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(q0 + u < cnt ? gv[u] : 0.0, q0 + u < cnt ? bv[u] : 0.0, s);
+            for (int u = 0; u < 8; ++u) dx = fma(wq[u], xq[u], dx);
         }
-        return s;
+        if (i >= n) dx *= ieps;
+        S[L->XV + i] = (pass == 0 ? (i < n ? S[L->X0 + i] : 0.0) : S[L->XV + i]) + dx;
     }
 };
 
@@ -544,15 +406,9 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     Trow.zero_from(0);
     Tcol.zero_from(0);
     GA.zero_from(0);
-    int status = notspd ? 3 : (a.limits_crossed ? 2 : 0);
-    int iters = 0, k = 0;
-    int act = 0;       // slot i < k: compact row
-    double sgn = 1.0;  // its sign
-    double lam = 0.0;  // its multiplier
-    bool aeq = false;  // it is an equality
-    bool onact = false; // lane ci: row ci is in the active set
-    int rounds = 0;
-    if (status == 0) {
+    GiState gs; // slots: act = compact row
+    gs.status = notspd ? 3 : (a.limits_crossed ? 2 : 0);
+    if (gs.status == 0) {
         // The 12 equality rows in one batch. Lane r < 12 holds row r of Gamma_EE; a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane
         // c then forward-substitutes column c of T = L^-1 against the broadcast rows of L, and
@@ -610,186 +466,23 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
             GA.put(q, kind != 0, kind != 0 ? S[L.GM + ci * L.GS + eq_row(q, NJ)] : 0.0);
         if (kind != 0) s_i += GA.dot(S + L.RV, 12);
         if (i < 12) {
-            act = er;
-            aeq = true;
-            lam = lm;
+            gs.act = er;
+            gs.aeq = true;
+            gs.lam = lm;
         }
-        onact = ci < 6 || (ci >= NJ && ci < NJ + 6);
-        k = 12;
-        iters = 1;
-        if (sing) status = 3; // dependent equality rows: the spec's level 1 is ill-posed
+        gs.onact = ci < 6 || (ci >= NJ && ci < NJ + 6);
+        gs.k = 12;
+        gs.iters = 1;
+        if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
         __syncthreads();
     }
-    bool need_select = true, dirty = true;
-    int cp = 0;
-    double sgp = 1.0, bnd = 0.0, lamp = 0.0;
-    const int maxit = a.max_iter;
-    bool go = status == 0;
-    while (go) {
-        if (need_select) {
-            double v = -1.0;
-            if (kind == 2 && !onact) {
-                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
-                const double viol = fmax(lo - s_i, s_i - hi);
-                if (viol > tol) v = viol / nrm;
-            }
-            int pi = i;
-            iargmax<64>(v, pi);
-            if (!(v > 0.0)) {
-                // no violated row: x is current unless steps were taken since the last
-                // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on the
-                // active set, and re-check every row with the exact activities
-                if (!dirty || rounds >= 3) break;
-                ++rounds;
-                dirty = false;
-                const double lo_a = __shfl(lo, act), hi_a = __shfl(hi, act); // all lanes active
-                S[L.RV + i] = i < k ? sgn * lam : 0.0;
-                S[L.AC + i] = (double)act;
-                __syncthreads();
-                for (int pass = 0; pass < 3; ++pass) {
-                    if (pass > 0) {
-                        // residual of the active rows, exact in x-space; correction through T
-                        const double res = i < k ? sgn * ((sgn > 0.0 ? lo_a : hi_a) - activity<NQ>(S, L, act, n, nf)) : 0.0;
-                        S[L.VV + i] = res;
-                        __syncthreads();
-                        const double y = Trow.dot(S + L.VV, k);
-                        S[L.LV + i] = i < k ? y : 0.0;
-                        __syncthreads();
-                        const double dl = i < k ? Tcol.dot(S + L.LV, k) : 0.0;
-                        lam += dl;
-                        S[L.RV + i] = i < k ? sgn * dl : 0.0;
-                        __syncthreads();
-                    }
-                    if (i < L.NX) { // x += H^-1 A_A^T (sgn dlam), slots in chunks of 8 loads
-                        double dx = 0.0;
-                        const int fi = i - n;
-                        for (int q0 = 0; q0 < k; q0 += 8) {
-                            int cq[8];
-                            double wq[8], xq[8];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                cq[u] = q0 + u < k ? (int)S[L.AC + q0 + u] : 0;
-                                wq[u] = q0 + u < k ? S[L.RV + q0 + u] : 0.0;
-                            }
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const int c = cq[u] < NJ + 6 ? cq[u] : 0;
-                                xq[u] = i < n ? (cq[u] < NJ + 6 ? S[L.XT + c * L.QS + i] : 0.0)
-                                              : fcoef(S, L, cq[u], fi < 0 ? 0 : fi);
-                            }
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) dx = fma(wq[u], xq[u], dx);
-                        }
-                        if (i >= n) dx *= ieps;
-                        S[L.XV + i] = (pass == 0 ? (i < n ? S[L.X0 + i] : 0.0) : S[L.XV + i]) + dx;
-                    }
-                    __syncthreads();
-                }
-                if (kind != 0) s_i = activity<NQ>(S, L, ci, n, nf);
-                continue;
-            }
-            cp = pi;
-            const double vl = __shfl(lo - s_i, cp), vh = __shfl(s_i - hi, cp);
-            sgp = vl > vh ? 1.0 : -1.0;
-            bnd = sgp > 0.0 ? __shfl(lo, cp) : __shfl(hi, cp);
-            lamp = 0.0;
-        }
-        if (++iters > maxit) {
-            status = 1;
-            break;
-        }
-        dirty = true;
-        // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
-        const double gpp = S[L.GM + cp * L.GS + cp];
-        S[L.VV + i] = i < k ? sgn * sgp * S[L.GM + act * L.GS + cp] : 0.0;
-        S[L.AC + i] = (double)act;
-        __syncthreads();
-        const double l = i < k ? Trow.dot(S + L.VV, k) : 0.0;
-        S[L.LV + i] = l;
-        __syncthreads();
-        const double r = i < k ? Tcol.dot(S + L.LV, k) : 0.0;
-        const double d2 = gpp - isum<64>(l * l);
-        S[L.RV + i] = i < k ? sgn * r : 0.0;
-        __syncthreads();
-        const double gjp = (kind != 0) ? S[L.GM + ci * L.GS + cp] : 0.0;
-        const double ds = (kind != 0) ? sgp * gjp - GA.dot(S + L.RV, k) : 0.0;
-        const double zz = sgp * __shfl(ds, cp);
-        const double slack = sgp * (__shfl(s_i, cp) - bnd); // < 0: violated
-        const double rmax = imax<64>(i < k ? fabs(r) : 0.0);
-        double cand = (i < k && !aeq && r > 1e-13 * rmax) ? lam / r : kInf;
-        int blk = i;
-        iargmin<64>(cand, blk);
-        const double t1 = cand;
-        const double t2 = (zz > 1e-14 * gpp) ? -slack / zz : kInf;
-        if (t1 >= kInf && t2 >= kInf) {
-            status = 2; // no feasible point with level 0 at b_w (level-0 repair: next)
-            break;
-        }
-        if (t2 <= t1 && k >= KM) { // cannot happen for independent rows; guard the storage
-            status = 3;
-            break;
-        }
-        const double t = fmin(t1, t2);
-        s_i = fma(t, ds, s_i);
-        if (i < k) lam = fma(-t, r, lam);
-        lamp += t;
-        if (t2 <= t1) { // add cp: T row k = [-(T^T l)^T / d, 1/d]
-            const double id = frsq(d2 > 0.0 ? d2 : zz);
-            const double tk = i < k ? -r * id : (i == k ? id : 0.0);
-            Tcol.put_dyn(k, i <= k, tk);
-            GA.put_dyn(k, kind != 0, gjp);
-            S[L.WV + i] = tk;
-            __syncthreads();
-            Trow.load_if(i == k, S + L.WV, k + 1);
-            if (i == k) {
-                act = cp;
-                sgn = sgp;
-                lam = lamp;
-                aeq = false;
-            }
-            if (i == cp) onact = true;
-            ++k;
-            need_select = true;
-            __syncthreads();
-        } else { // drop slot blk (its multiplier reached zero), keep stepping on cp
-            const int cb = __shfl(act, blk);
-            if (i == cb) onact = false;
-            const int na = __shfl(act, i + 1);
-            const double ns = __shfl(sgn, i + 1), nl = __shfl(lam, i + 1);
-            const bool ne = __shfl(aeq ? 1 : 0, i + 1) != 0;
-            if (i >= blk) {
-                act = na;
-                sgn = ns;
-                lam = nl;
-                aeq = ne;
-            }
-            GA.shift_down(blk, k);
-            --k;
-            // rows and columns of T before blk stand; re-append the slots after it
-            Trow.zero_if(i >= blk);
-            Tcol.zero_from(blk);
-            __syncthreads();
-            for (int a2 = blk; a2 < k; ++a2) {
-                const int cq = __shfl(act, a2);
-                const double sq = __shfl(sgn, a2);
-                S[L.VV + i] = i < a2 ? sgn * sq * S[L.GM + act * L.GS + cq] : 0.0;
-                __syncthreads();
-                const double l2 = i < a2 ? Trow.dot(S + L.VV, a2) : 0.0;
-                S[L.LV + i] = l2;
-                __syncthreads();
-                const double r2 = i < a2 ? Tcol.dot(S + L.LV, a2) : 0.0;
-                const double e2 = S[L.GM + cq * L.GS + cq] - isum<64>(l2 * l2);
-                const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
-                const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
-                Tcol.put_dyn(a2, i <= a2, tk2);
-                S[L.WV + i] = tk2;
-                __syncthreads();
-                Trow.load_if(i == a2, S + L.WV, a2 + 1);
-                __syncthreads();
-            }
-            need_select = false;
-        }
+    {
+        const ContactGi<NQ> pb{S, &L, n, nf, i, ieps};
+        dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
+                    a.max_iter);
     }
+    int status = gs.status;
+    const int iters = gs.iters;
 
     // ------------------------------------------------------------------ 7. outputs
     __syncthreads();
@@ -828,7 +521,7 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     }
     WBQ_STAMP(6);
 #ifdef WBQ_STAMPS
-    if (i == 0 && a.stamps) a.stamps[b * kStamps + 7] = rounds;
+    if (i == 0 && a.stamps) a.stamps[b * kStamps + 7] = gs.rounds;
 #endif
 }
 

@@ -1,0 +1,387 @@
+// dual_gi.h -- Goldfarb-Idnani dual active set carried in constraint space, one lane per
+// constraint row (gfx950, wave64, fp64). Shared by the contact-form kernel and the QPPVM
+// W1 = M kernel: both solve
+//   min 0.5 (x - x0)^T H (x - x0)   s.t.  lo_j <= a_j x <= hi_j  (lo_j == hi_j: equality)
+// knowing only Gamma = A H^-1 A^T (m x m), the activities s = A x and H^-1 A^T. The
+// active-set Gram Gamma_AA = L L^T is kept as T = L^-1 (an add appends one row of T in
+// closed form, a drop re-appends the rows after it) and x is rebuilt from the multipliers,
+// x = x0 + H^-1 A_A^T lambda, only when the active set settles; two steps of iterative
+// refinement on the final active set (residuals exact in x-space) and a re-check of every
+// row follow (the algorithm the oracle restates in
+// oracle/wbq_oracle_contact.c and oracle/wbq_oracle.c).
+//
+// The problem supplies a policy P with
+//   double gamma(int r, int c) const      Gamma[r][c]
+//   double activity(int r) const          a_r . x at x = the current rebuilt x (LDS)
+//   void rebuild(int pass, int k) const   x = (pass 0: x0, else x) + H^-1 A^T w with the
+//                                          weights w in RV[0..k) on the rows AC[0..k)
+// and the LDS offsets of five 72-double scratch vectors (VV, LV, RV, WV, AC).
+#pragma once
+#include "wbq_device.h"
+
+namespace wbq {
+
+// Per-lane vector of active-slot values (T rows, T columns, Gamma columns of the active
+// set): in registers (KM static; dynamic writes by select) or one LDS row per lane, whose
+// dots load in chunks of 8 independent reads. Either way the loads of a dot issue back to
+// back instead of one dependent LDS round trip per term.
+template <int KM, bool REG>
+struct SlotVec;
+
+template <int KM>
+struct SlotVec<KM, true> {
+    double v[KM];
+    __device__ void bind(double *, int) {}
+    __device__ void zero_from(int c)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = (j >= c) ? 0.0 : v[j];
+    }
+    __device__ void zero_if(bool cond)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = cond ? 0.0 : v[j];
+    }
+    __device__ void put(int c, bool cond, double x) { v[c] = cond ? x : v[c]; } // c static after unrolling
+    __device__ void put_dyn(int c, bool cond, double x)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) v[j] = (cond && j == c) ? x : v[j];
+    }
+    __device__ void load_if(bool cond, const double *src, int cnt)
+    {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double w = src[j];
+            v[j] = (cond && j < cnt) ? w : v[j];
+        }
+    }
+    __device__ void shift_down(int c, int cnt) // v[j] = v[j + 1] for c <= j < cnt - 1
+    {
+#pragma unroll
+        for (int j = 0; j + 1 < KM; ++j) v[j] = (j >= c && j + 1 < cnt) ? v[j + 1] : v[j];
+    }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double bj = b[j];
+            s = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s);
+        }
+        return s;
+    }
+};
+
+template <int KM>
+struct SlotVec<KM, false> {
+    double *p;
+    int cap;
+    __device__ void bind(double *row, int capacity)
+    {
+        p = row;
+        cap = capacity;
+    }
+    __device__ void zero_from(int c)
+    {
+        for (int j = c; j < cap; ++j) p[j] = 0.0;
+    }
+    __device__ void zero_if(bool cond)
+    {
+        if (cond)
+            for (int j = 0; j < cap; ++j) p[j] = 0.0;
+    }
+    __device__ void put(int c, bool cond, double x)
+    {
+        if (cond) p[c] = x;
+    }
+    __device__ void put_dyn(int c, bool cond, double x)
+    {
+        if (cond) p[c] = x;
+    }
+    __device__ void load_if(bool cond, const double *src, int cnt)
+    {
+        if (cond)
+            for (int j = 0; j < cnt; ++j) p[j] = src[j];
+    }
+    __device__ void shift_down(int c, int cnt)
+    {
+        for (int j = c; j + 1 < cnt; ++j) p[j] = p[j + 1];
+    }
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int c0 = 0; c0 < cnt; c0 += 8) {
+            double pv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                pv[u] = p[c0 + u];
+                bv[u] = b[c0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+        }
+        return s;
+    }
+};
+
+// value of v in lane `lane` (uniform), as a scalar broadcast (v_readlane, no LDS)
+__device__ __forceinline__ double bcast(double v, int lane)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+// LDS views with no storage of their own: column a of T read from the T rows (lane a:
+// T[c][a] = TT[c TS + a]), and Gamma[j][act_q] gathered from lane j's Gamma row through the
+// slot list AC; chunks of 8 independent loads. Their writes are no-ops (the data is in the
+// T rows and in Gamma).
+struct TColView {
+    const double *tt;
+    int ts;
+    __device__ void bind(const double *col, int stride)
+    {
+        tt = col;
+        ts = stride;
+    }
+    __device__ void zero_from(int) {}
+    __device__ void put(int, bool, double) {}
+    __device__ void put_dyn(int, bool, double) {}
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int c0 = 0; c0 < cnt; c0 += 8) {
+            double pv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                pv[u] = tt[(c0 + u) * ts];
+                bv[u] = b[c0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+        }
+        return s;
+    }
+};
+
+struct GAView {
+    const double *grow, *ac;
+    __device__ void bind(const double *row, const double *slots)
+    {
+        grow = row;
+        ac = slots;
+    }
+    __device__ void zero_from(int) {}
+    __device__ void put(int, bool, double) {}
+    __device__ void put_dyn(int, bool, double) {}
+    __device__ void shift_down(int, int) {}
+    __device__ double dot(const double *b, int cnt) const
+    {
+        double s = 0.0;
+        for (int q0 = 0; q0 < cnt; q0 += 8) {
+            int cq[8];
+            double bv[8], gv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cq[u] = q0 + u < cnt ? (int)ac[q0 + u] : 0;
+                bv[u] = b[q0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) gv[u] = grow[cq[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fma(q0 + u < cnt ? gv[u] : 0.0, q0 + u < cnt ? bv[u] : 0.0, s);
+        }
+        return s;
+    }
+};
+
+constexpr int kGiRounds = 8;      // x rebuilds (each followed by a re-check of every row)
+constexpr double kGiDep = 1e-10; // dependent-row threshold on the Schur complement / Gamma_pp
+
+// LDS scratch vectors of the loop (72 doubles each: slot dots read 8 past the active count)
+struct GiVecs {
+    int VV, LV, RV, WV, AC;
+};
+
+// Lane state. Slot a (lane a < k) = the a-th active row: act (its index), sgn (normal =
+// sgn * a_act), lam (its multiplier), aeq (an equality: never dropped). Lane j (row j)
+// keeps onact = row j is active.
+struct GiState {
+    int k = 0, act = 0, iters = 0, status = 0, rounds = 0;
+    double sgn = 1.0, lam = 0.0;
+    bool aeq = false, onact = false;
+};
+
+// The loop itself (lane i = constraint row i; kind 0 disabled, 1 equality already in the
+// active set, 2 a row with limits [lo, hi], lo == hi an equality added when violated).
+// Statuses: 1 step cap, 2 no step exists (the rows are inconsistent: infeasible), 3 the slot
+// storage overflowed (dependent rows). On exit with status 0, x in LDS and s_i are exact.
+template <int KM, class P, class TrowT, class TcolT, class GAT>
+__device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V, int i, TrowT &Trow, TcolT &Tcol,
+                                        GAT &GA, int kind, double lo, double hi, double nrm, double &s_i, GiState &g,
+                                        int maxit)
+{
+    bool need_select = true, dirty = true;
+    int cp = 0;
+    double sgp = 1.0, bnd = 0.0, lamp = 0.0;
+    bool peq = false;
+    bool go = g.status == 0;
+    while (go) {
+        if (need_select) {
+            double v = -1.0;
+            if (kind == 2 && !g.onact) {
+                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                const double viol = fmax(lo - s_i, s_i - hi);
+                if (viol > tol) v = viol / nrm;
+            }
+            int pi = i;
+            iargmax<64>(v, pi);
+            if (!(v > 0.0)) {
+                // no violated row: x is current unless steps were taken since the last
+                // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on the
+                // active set, and re-check every row with the exact activities. A re-check
+                // that keeps finding rows the incremental activities missed is capped; x is
+                // stale then, so that is a failure (status 1), never a silent success.
+                if (!dirty) break;
+                if (g.rounds >= kGiRounds) {
+                    g.status = 1;
+                    break;
+                }
+                ++g.rounds;
+                dirty = false;
+                const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act); // all lanes active
+                S[V.RV + i] = i < g.k ? g.sgn * g.lam : 0.0;
+                S[V.AC + i] = (double)g.act;
+                __syncthreads();
+                for (int pass = 0; pass < 3; ++pass) {
+                    if (pass > 0) {
+                        // residual of the active rows, exact in x-space; correction through T
+                        const double res =
+                            i < g.k ? g.sgn * ((g.sgn > 0.0 ? lo_a : hi_a) - pb.activity(g.act)) : 0.0;
+                        S[V.VV + i] = res;
+                        __syncthreads();
+                        const double y = Trow.dot(S + V.VV, g.k);
+                        S[V.LV + i] = i < g.k ? y : 0.0;
+                        __syncthreads();
+                        const double dl = i < g.k ? Tcol.dot(S + V.LV, g.k) : 0.0;
+                        g.lam += dl;
+                        S[V.RV + i] = i < g.k ? g.sgn * dl : 0.0;
+                        __syncthreads();
+                    }
+                    pb.rebuild(pass, g.k);
+                    __syncthreads();
+                }
+                if (kind != 0) s_i = pb.activity(i);
+                continue;
+            }
+            cp = pi;
+            const double vl = __shfl(lo - s_i, cp), vh = __shfl(s_i - hi, cp);
+            sgp = vl > vh ? 1.0 : -1.0;
+            bnd = sgp > 0.0 ? __shfl(lo, cp) : __shfl(hi, cp);
+            peq = __shfl(lo == hi ? 1 : 0, cp) != 0;
+            lamp = 0.0;
+        }
+        if (++g.iters > maxit) {
+            g.status = 1;
+            break;
+        }
+        dirty = true;
+        // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
+        const double gpp = pb.gamma(cp, cp);
+        S[V.VV + i] = i < g.k ? g.sgn * sgp * pb.gamma(g.act, cp) : 0.0;
+        S[V.AC + i] = (double)g.act;
+        __syncthreads();
+        const double l = i < g.k ? Trow.dot(S + V.VV, g.k) : 0.0;
+        S[V.LV + i] = l;
+        __syncthreads();
+        const double r = i < g.k ? Tcol.dot(S + V.LV, g.k) : 0.0;
+        const double d2 = gpp - isum<64>(l * l);
+        S[V.RV + i] = i < g.k ? g.sgn * r : 0.0;
+        __syncthreads();
+        const double gjp = (kind != 0) ? pb.gamma(i, cp) : 0.0;
+        const double ds = (kind != 0) ? sgp * gjp - GA.dot(S + V.RV, g.k) : 0.0;
+        const double zz = sgp * __shfl(ds, cp);
+        const double slack = sgp * (__shfl(s_i, cp) - bnd); // < 0: violated
+        const double rmax = imax<64>(i < g.k ? fabs(r) : 0.0);
+        double cand = (i < g.k && !g.aeq && r > 1e-13 * rmax) ? g.lam / r : kInf;
+        int blk = i;
+        iargmin<64>(cand, blk);
+        const double t1 = cand;
+        // zz is the Schur complement of row cp against the active set, formed by cancellation:
+        // its roundoff is ~eps cond(Gamma_AA) gpp (1e-9 gpp at cond 1e7), so a row whose
+        // complement is below kGiDep gpp is dependent (no primal step), whatever its sign
+        const double t2 = (zz > kGiDep * gpp) ? -slack / zz : kInf;
+        if (t1 >= kInf && t2 >= kInf) {
+            g.status = 2; // no step: the rows cannot all be met
+            break;
+        }
+        if (t2 <= t1 && g.k >= KM) { // cannot happen for independent rows; guard the storage
+            g.status = 3;
+            break;
+        }
+        const double t = fmin(t1, t2);
+        s_i = fma(t, ds, s_i);
+        if (i < g.k) g.lam = fma(-t, r, g.lam);
+        lamp += t;
+        if (t2 <= t1) { // add cp: T row k = [-(T^T l)^T / d, 1/d]
+            const double id = frsq(d2 > 0.0 ? d2 : zz);
+            const double tk = i < g.k ? -r * id : (i == g.k ? id : 0.0);
+            Tcol.put_dyn(g.k, i <= g.k, tk);
+            GA.put_dyn(g.k, kind != 0, gjp);
+            S[V.WV + i] = tk;
+            __syncthreads();
+            Trow.load_if(i == g.k, S + V.WV, g.k + 1);
+            if (i == g.k) {
+                g.act = cp;
+                g.sgn = sgp;
+                g.lam = lamp;
+                g.aeq = peq;
+            }
+            if (i == cp) g.onact = true;
+            ++g.k;
+            need_select = true;
+            __syncthreads();
+        } else { // drop slot blk (its multiplier reached zero), keep stepping on cp
+            const int cb = __shfl(g.act, blk);
+            if (i == cb) g.onact = false;
+            const int na = __shfl(g.act, i + 1);
+            const double ns = __shfl(g.sgn, i + 1), nl = __shfl(g.lam, i + 1);
+            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1) != 0;
+            if (i >= blk) {
+                g.act = na;
+                g.sgn = ns;
+                g.lam = nl;
+                g.aeq = ne;
+            }
+            GA.shift_down(blk, g.k);
+            --g.k;
+            // rows and columns of T before blk stand; re-append the slots after it
+            Trow.zero_if(i >= blk);
+            Tcol.zero_from(blk);
+            __syncthreads();
+            for (int a2 = blk; a2 < g.k; ++a2) {
+                const int cq = __shfl(g.act, a2);
+                const double sq = __shfl(g.sgn, a2);
+                S[V.VV + i] = i < a2 ? g.sgn * sq * pb.gamma(g.act, cq) : 0.0;
+                __syncthreads();
+                const double l2 = i < a2 ? Trow.dot(S + V.VV, a2) : 0.0;
+                S[V.LV + i] = l2;
+                __syncthreads();
+                const double r2 = i < a2 ? Tcol.dot(S + V.LV, a2) : 0.0;
+                const double e2 = pb.gamma(cq, cq) - isum<64>(l2 * l2);
+                const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
+                const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
+                Tcol.put_dyn(a2, i <= a2, tk2);
+                S[V.WV + i] = tk2;
+                __syncthreads();
+                Trow.load_if(i == a2, S + V.WV, a2 + 1);
+                __syncthreads();
+            }
+            need_select = false;
+        }
+    }
+}
+
+}  // namespace wbq

@@ -36,6 +36,7 @@
 // M must be symmetric (it is read column-wise as rows).
 #include "wbq_kernels.h"
 #include "wbq_device.h"
+#include "qppvm_repair.h"
 
 #include <math.h>
 
@@ -64,25 +65,6 @@ struct FastLayout {
         GR = RES + m0;           // Gram G G^T, lower triangle [m0][kM0Max]
         PS = GR + m0 * kM0Max;   // poses [T][24]
         SIZE = (PS + 24 * T + 1) & ~1;
-    }
-};
-
-template <int NP>
-struct ActiveLayout {
-    static constexpr bool MREG = (NP == 32); // M rows and T rows in VGPRs (else in LDS)
-    static constexpr int RS = NP + 1;
-    int QA, MA, TT, U, D1, D1B, NV, BC, SIZE;
-    __host__ __device__ ActiveLayout(int, int)
-    {
-        QA = 0;                           // Q1^T rows [NP][RS]
-        MA = QA + NP * RS;                // M rows (NP == 64)
-        TT = MA + (MREG ? 0 : NP * RS);   // T = R_II^-1 rows (NP == 64)
-        U = TT + (MREG ? 0 : NP * RS);    // u
-        D1 = U + NP;                      // d1 = Q1^T n_p, zero-padded to 2 NP
-        D1B = D1 + 2 * NP;                // second Gram-Schmidt pass
-        NV = D1B + NP;                    // n_p
-        BC = NV + NP;                     // broadcast scratch
-        SIZE = (BC + NP + 1) & ~1;
     }
 };
 
@@ -132,446 +114,6 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
     return z;
 }
 
-
-// ============================================================== level-0 repair
-// Packed lower triangle index (row-major).
-__host__ __device__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
-
-// Diagonal-pivoted Cholesky of a PSD K x K Gram held redundantly per lane (packed lower,
-// original row order; rows >= m ignored): P Gram P^T = L L^T, rank k = number of pivots
-// above tol * max diagonal. Pivoting keeps the left-over Schur diagonal at roundoff level,
-// so the rank decision is reliable (without it, a small genuine pivot inflates the
-// dependent rows' pivots far above roundoff). Static register indices throughout: the
-// dynamic pivot is applied with select chains.
-template <int K>
-struct PivChol {
-    static constexpr int T = K * (K + 1) / 2;
-    int k;           // rank
-    int piv[K];      // original row of pivot c (c < k)
-    bool used[K];    // row pivoted (or >= m)
-    double Lp[T];    // L restricted to the pivot rows, step order (packed lower)
-    double Lo[K][K]; // L row of every original row (columns = pivot steps)
-
-    __device__ static double gsym(const double (&g)[T], int i, int p)
-    {
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) v = (q == p) ? g[i >= q ? tri(i, q) : tri(q, i)] : v;
-        return v;
-    }
-
-    __device__ void factor(const double (&g)[T], int m, double tol)
-    {
-        double d[K], dmx = 0.0;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            d[i] = i < m ? g[tri(i, i)] : 0.0;
-            dmx = fmax(dmx, d[i]);
-            used[i] = i >= m;
-            piv[i] = 0;
-#pragma unroll
-            for (int c = 0; c < K; ++c) Lo[i][c] = 0.0;
-        }
-#pragma unroll
-        for (int t = 0; t < T; ++t) Lp[t] = 0.0;
-        k = 0;
-        bool stop = false;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            int p = 0;
-            double best = -1.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-                if (!used[i] && d[i] > best) {
-                    best = d[i];
-                    p = i;
-                }
-            stop = stop || !(best > tol * dmx);
-            if (!stop) {
-                piv[c] = p;
-                k = c + 1;
-                const double lpp = sqrt(best), il = 1.0 / lpp;
-                double rp[K];
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int i = 0; i < K; ++i) v = (i == p) ? Lo[i][j] : v;
-                    rp[j] = v;
-                }
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    used[i] = used[i] || i == p;
-                    if (!used[i]) {
-                        double v = gsym(g, i, p);
-#pragma unroll
-                        for (int j = 0; j < c; ++j) v = fma(-Lo[i][j], rp[j], v);
-                        v *= il;
-                        Lo[i][c] = v;
-                        d[i] = fma(-v, v, d[i]);
-                    }
-                    if (i == p) Lo[i][c] = lpp;
-                }
-#pragma unroll
-                for (int j = 0; j < c; ++j) Lp[tri(c, j)] = rp[j];
-                Lp[tri(c, c)] = lpp;
-            }
-        }
-    }
-
-    // Weights w (original row order) of the minimum-norm least-squares solution z = A^T w of
-    // A z = r, where Gram = A A^T (rows m..K-1 absent). With C = L_D L_P^-1 relating the
-    // dependent rows D to the pivot rows P:
-    //   s = (I + C^T C)^-1 (r_P + C^T r_D),  w_P = Gram_PP^-1 s,  w_D = 0
-    // (the oracle does this solve with an SVD: oracle/wbq_oracle.c:minnorm_ls).
-    __device__ void solve(const double (&r)[K], int m, double (&w)[K]) const
-    {
-        double rh[K], H[T];
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            double v = 0.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i) v = (c < k && piv[c] == i) ? r[i] : v;
-            rh[c] = v;
-        }
-#pragma unroll
-        for (int p = 0; p < K; ++p)
-#pragma unroll
-            for (int q = 0; q <= p; ++q) H[tri(p, q)] = p == q ? 1.0 : 0.0;
-        double ild[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) ild[c] = c < k ? 1.0 / Lp[tri(c, c)] : 0.0;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            bool dep = i < m;
-#pragma unroll
-            for (int c = 0; c < K; ++c) dep = dep && !(c < k && piv[c] == i);
-            if (dep) {
-                double ci[K];
-#pragma unroll
-                for (int c = K - 1; c >= 0; --c) {
-                    double v = Lo[i][c];
-#pragma unroll
-                    for (int c2 = c + 1; c2 < K; ++c2) v = fma(-Lp[tri(c2, c)], ci[c2], v);
-                    ci[c] = v * ild[c];
-                }
-#pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    rh[p] = fma(ci[p], r[i], rh[p]);
-#pragma unroll
-                    for (int q = 0; q <= p; ++q) H[tri(p, q)] = fma(ci[p], ci[q], H[tri(p, q)]);
-                }
-            }
-        }
-        double ih[K]; // Cholesky of H (SPD, well conditioned: |C| is bounded under pivoting)
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            double dd = H[tri(c, c)];
-#pragma unroll
-            for (int j = 0; j < c; ++j) dd = fma(-H[tri(c, j)], H[tri(c, j)], dd);
-            ih[c] = 1.0 / sqrt(dd);
-            H[tri(c, c)] = dd * ih[c];
-#pragma unroll
-            for (int r2 = c + 1; r2 < K; ++r2) {
-                double t = H[tri(r2, c)];
-#pragma unroll
-                for (int j = 0; j < c; ++j) t = fma(-H[tri(r2, j)], H[tri(c, j)], t);
-                H[tri(r2, c)] = t * ih[c];
-            }
-        }
-        double sv[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            double v = rh[c];
-#pragma unroll
-            for (int j = 0; j < c; ++j) v = fma(-H[tri(c, j)], sv[j], v);
-            sv[c] = v * ih[c];
-        }
-#pragma unroll
-        for (int c = K - 1; c >= 0; --c) {
-            double v = sv[c];
-#pragma unroll
-            for (int j = c + 1; j < K; ++j) v = fma(-H[tri(j, c)], sv[j], v);
-            sv[c] = v * ih[c];
-        }
-        // w_P = L_P^-T L_P^-1 s
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            double v = sv[c];
-#pragma unroll
-            for (int j = 0; j < c; ++j) v = fma(-Lp[tri(c, j)], sv[j], v);
-            sv[c] = v * ild[c];
-        }
-#pragma unroll
-        for (int c = K - 1; c >= 0; --c) {
-            double v = sv[c];
-#pragma unroll
-            for (int j = c + 1; j < K; ++j) v = fma(-Lp[tri(j, c)], sv[j], v);
-            sv[c] = v * ild[c];
-        }
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            double v = 0.0;
-#pragma unroll
-            for (int c = 0; c < K; ++c) v = (c < k && piv[c] == i) ? sv[c] : v;
-            w[i] = v;
-        }
-    }
-
-    // Orthonormal basis of range(A^T) (lane-distributed rows): q_c = (L_P^-1 a_P)[c], c < k
-    __device__ void basis(const double (&acol)[K], double (&q)[K]) const
-    {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            double v = 0.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i) v = (piv[c] == i) ? acol[i] : v;
-#pragma unroll
-            for (int j = 0; j < c; ++j) v = fma(-Lp[tri(c, j)], q[j], v);
-            q[c] = c < k ? v / Lp[tri(c, c)] : 0.0;
-        }
-    }
-};
-
-template <int NP, int K>
-__device__ __forceinline__ void isum_vec(double (&v)[K])
-{
-#pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1)
-#pragma unroll
-        for (int c = 0; c < K; ++c) v[c] += __shfl_xor(v[c], m, NP);
-}
-
-struct RepairOut {
-    double lo, hi, u; // (possibly pinned) limits and the new u of this lane
-    int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
-    bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
-};
-
-// Level-0 repair for the instances with rep set (every lane of the wave calls this; the
-// instance -> lane mapping is the kernel's). Level 0 in x-space is
-//   min 0.5 ||A0 x - b0||^2  s.t. lo <= x <= hi,   A0 = G M^-1   (QPPVMPlugin.cpp:129-152,177)
-// Solved by BVLS (Stark-Parker), the algorithm of oracle/wbq_oracle.c:wbq_ref_level0, with
-// lane i owning column a_i = (M^-1 G^T)_i (block Gauss-Jordan on the M rows, reloaded from
-// HBM/L2: this path is rare). Then y* = A0 x*, every variable the level-0 gradient
-// w = A0^T (b0 - y*) holds at a bound is pinned there (lo = hi, as wbq_ref_qppvm_one does),
-// and u is reset to the least-distance point of G u = y*, with the Q1 rows (orthonormal
-// basis of range(G^T), zero rows past its rank) in LDS for a fresh dual active set.
-// Not inlined: its registers do not weigh on the active-set loop.
-template <int NP, int M0>
-__device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff, long b, int i, bool rep, double lo,
-                                                double hi, bool warm)
-{
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    double *S = smem + soff;
-    constexpr int RS = NP + 1;
-    constexpr int NT = M0 * (M0 + 1) / 2;
-    const ActiveLayout<NP> L(a.ntasks, a.m0);
-    const int n = a.n, m0 = a.m0;
-    const int ic = i < n ? i : n - 1;
-    const bool row = rep && i < n;
-    RepairOut out{lo, hi, 0.0, 0, 0, false};
-    double gcol[M0], acol[M0], b0v[M0];
-    const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
-#pragma unroll
-    for (int c = 0; c < M0; ++c) {
-        const bool on = rep && c < m0;
-        const int rr = on ? a.row_sel[c] : 0;
-        gcol[c] = (on && row) ? a.J[(b * a.ntasks * 6 + rr) * n + ic] : 0.0;
-        b0v[c] = on ? a.b0_scr[b * kM0Max + c] : 0.0;
-        acol[c] = gcol[c];
-    }
-    // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
-    // are rebuilt below)
-    {
-        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, (long)a.B * n * n);
-        const int moff = (int)(8 * (b * n * n + ic));
-        double A[NP];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
-        __syncthreads();
-        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 8 * NP);
-    }
-    WBQ_STAMP(9);
-    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)
-    double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
-    int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
-    if (row && warm) {    // warm start: the bound state of the last repair (any state is valid)
-        const int w = a.ws_state[b * NP + i];
-        st = (w < 0) ? -1 : (w > 0 ? 1 : 0);
-        xv = st < 0 ? lo : (st > 0 ? hi : xv);
-    }
-    if (row && lo == hi) {
-        st = -1;
-        xv = lo;
-    }
-    bool ex = false; // excluded from the next KKT pick (Stark-Parker anti-cycling)
-    double abm = 0.0;
-#pragma unroll
-    for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
-    const double wtb = fabs(abm);
-    abm = fmax(1.0, imax<NP>(wtb));
-    const double pintol = 1e-9 * abm;
-    int freed = -1, it = 0;
-    const int maxit = 50 * n + 100;
-    bool outer = rep;
-    while (__any(outer)) {
-        bool inner = outer;
-        while (__any(inner)) {
-            if (inner) ++it;
-            const bool fr = inner && st == 0;
-            double rv[M0], gp[NT];
-#pragma unroll
-            for (int c = 0; c < M0; ++c) rv[c] = (st == -1 || st == 1) ? acol[c] * xv : 0.0;
-#pragma unroll
-            for (int p = 0; p < M0; ++p)
-#pragma unroll
-                for (int c = 0; c <= p; ++c) gp[tri(p, c)] = fr ? acol[p] * acol[c] : 0.0;
-            isum_vec<NP, M0>(rv);
-            isum_vec<NP, NT>(gp);
-            const double kfree = isum<NP>(fr ? 1.0 : 0.0);
-#pragma unroll
-            for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
-            // minimum-norm least squares on the free set: z = A_F^T w
-            double wv[M0];
-            {
-                PivChol<M0> pc;
-                pc.factor(gp, m0, 1e-12);
-                pc.solve(rv, m0, wv);
-            }
-            double z = 0.0;
-#pragma unroll
-            for (int c = 0; c < M0; ++c) z = fma(acol[c], wv[c], z);
-            // interpolate back into the box: blocking variable = smallest step fraction < 1
-            double al = kInf;
-            if (fr) {
-                const double step = z - xv;
-                if (z < lo && step < 0.0) al = (lo - xv) / step;
-                else if (z > hi && step > 0.0) al = (hi - xv) / step;
-                if (!(al < 1.0)) al = kInf;
-            }
-            int jb = i;
-            iargmin<NP>(al, jb);
-            if (inner) {
-                if (!(kfree > 0.0)) {
-                    inner = false;
-                } else if (al >= kInf) { // z inside the box: take it
-                    if (fr) xv = z;
-                    freed = -1;
-                    ex = false; // progress: exclusions expire
-                    inner = false;
-                } else {
-                    const double alpha = fmax(al, 0.0);
-                    if (jb == freed && alpha == 0.0) {
-                        // the variable just freed wants back through its bound: re-bind, exclude
-                        if (i == jb) {
-                            ex = true;
-                            st = (z < lo) ? -1 : 1;
-                            xv = st < 0 ? lo : hi;
-                        }
-                        inner = false;
-                    } else {
-                        ex = false; // progress: exclusions expire
-                        if (fr) {
-                            xv = fma(alpha, z - xv, xv);
-                            const double tl = 1e-14 * fmax(1.0, fabs(lo)), tu = 1e-14 * fmax(1.0, fabs(hi));
-                            if (i == jb) st = (z < lo) ? -1 : 1;
-                            else if (xv <= lo + tl && z < lo) st = -1;
-                            else if (xv >= hi - tu && z > hi) st = 1;
-                            if (st == -1) xv = lo;
-                            if (st == 1) xv = hi;
-                        }
-                    }
-                    freed = -1;
-                    if (it >= maxit) inner = false;
-                }
-            }
-        }
-        // KKT on the bound variables: w = A0^T (b0 - A0 x)
-        double rf[M0];
-#pragma unroll
-        for (int c = 0; c < M0; ++c) rf[c] = acol[c] * xv;
-        isum_vec<NP, M0>(rf);
-        double w = 0.0, wx = 0.0;
-#pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            w = fma(acol[c], b0v[c] - rf[c], w);
-            wx = fma(acol[c], rf[c], wx);
-        }
-        // KKT tolerance relative to the terms of w = A0^T b0 - A0^T A0 x (with b0 ~ 0 the
-        // second dominates, and its roundoff must not read as a descent direction)
-        const double wtol = 1e-11 * fmax(abm, imax<NP>(fmax(wtb, fabs(wx))));
-        double v = -kInf;
-        if (outer && (st == -1 || st == 1) && !ex && lo != hi) v = st < 0 ? w : -w;
-        int best = i;
-        iargmax<NP>(v, best);
-        if (outer) {
-            if (!(v > wtol)) {
-                outer = false;
-            } else if (it >= maxit) {
-                out.status = 1;
-                outer = false;
-            } else {
-                if (i == best) st = 0; // exclusions persist until the inner loop makes progress
-                freed = best;
-            }
-        }
-    }
-    WBQ_STAMP(10);
-    // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
-    if (row) a.ws_state[b * NP + i] = (signed char)(st == 2 ? 0 : st);
-    double ys[M0];
-#pragma unroll
-    for (int c = 0; c < M0; ++c) ys[c] = acol[c] * xv;
-    isum_vec<NP, M0>(ys);
-    {
-        double gap = 0.0, bmx = 1.0;
-#pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            gap = fmax(gap, fabs(ys[c] - b0v[c]));
-            bmx = fmax(bmx, fabs(b0v[c]));
-        }
-        out.l0inf = rep && gap > 1e-9 * bmx;
-    }
-    if (row) {
-        double w = 0.0;
-#pragma unroll
-        for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - ys[c], w);
-        if (w > pintol) out.lo = hi;       // pinned at the upper bound
-        else if (w < -pintol) out.hi = lo; // pinned at the lower bound
-    }
-    double gg[NT], rr[M0];
-#pragma unroll
-    for (int p = 0; p < M0; ++p) {
-        rr[p] = gcol[p] * uimp;
-#pragma unroll
-        for (int c = 0; c <= p; ++c) gg[tri(p, c)] = gcol[p] * gcol[c];
-    }
-    isum_vec<NP, M0>(rr);
-    isum_vec<NP, NT>(gg);
-#pragma unroll
-    for (int c = 0; c < M0; ++c) rr[c] = ys[c] - rr[c]; // y* - G u_imp (consistent)
-    double q1[M0], cv[M0];
-    {
-        PivChol<M0> pc;
-        pc.factor(gg, m0, 1e-12);
-        pc.solve(rr, m0, cv);
-        pc.basis(gcol, q1);
-    }
-    double un = uimp;
-#pragma unroll
-    for (int c = 0; c < M0; ++c) un = fma(gcol[c], cv[c], un);
-    out.u = rep ? un : 0.0;
-    __syncthreads(); // Gauss-Jordan scratch in QA is dead
-    if (rep) {
-#pragma unroll
-        for (int c = 0; c < NP; ++c) S[L.QA + c * RS + i] = (c < M0 && c < m0) ? q1[c < M0 ? c : 0] : 0.0;
-    }
-    out.it = rep ? it : 0;
-    return out;
-}
 
 // ============================================================== active-set path
 // Goldfarb-Idnani dual active set on the torque bounds (QPPVMPlugin.cpp:203-205 limits) in
@@ -750,16 +292,6 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         }
     }
     return Mr.dot(S + L.U, NP);
-}
-
-// Work lists: the producing kernel appends every instance that needs a follow-up kernel
-// (atomic counter work[epoch*2 + 0] / [+1], lists wl[0..B) / wl[B..2B)), and the follow-up
-// kernels run a small grid-stride grid over the list. Without work a launch is one
-// broadcast load per block of at most kFollowGrid blocks, instead of a batch-sized grid.
-__device__ __forceinline__ void wl_push(const QppvmArgs &a, int list, long b)
-{
-    const int idx = atomicAdd(&a.work[a.epoch * 2 + list], 1);
-    a.wl[(long)list * a.B + idx] = (int)b;
 }
 
 // Active-set kernel (NP = 64; NP = 32 runs it inline in the fast kernel): instances parked
@@ -1193,11 +725,6 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
     return hipGetLastError();
 }
 
-// Follow-up grid cap: 2 waves per SIMD over the whole chip (launch cost measured independent of
-// the grid size, scripts/launch_probe.hip; a smaller cap starves a solve where many instances
-// need the repair, e.g. diverging MPC rollouts)
-constexpr unsigned kFollowGrid = 2048;
-
 template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
@@ -1226,6 +753,7 @@ bool qppvm_single_launch(int) { return false; }
 
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
+    if (a.joint_weight == 1) return launch_qppvm_w1m(a, stream, mid);
     if (a.n <= 32) return a.m0 <= 6 ? launch_np<32, 6>(a, stream, mid) : launch_np<32, kM0Max>(a, stream, mid);
     return a.m0 <= 6 ? launch_np<64, 6>(a, stream, mid) : launch_np<64, kM0Max>(a, stream, mid);
 }

@@ -194,7 +194,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     if (d.n < 1 || d.n > 64 || d.ntasks < 1 || d.ntasks > wbq::kTMax || d.max_batch < 1)
         return WBQ_E_INVALID;
     if (d.select_mode != WBQ_SELECT_SUBTASK && d.select_mode != WBQ_SELECT_TASK) return WBQ_E_INVALID;
-    if (d.joint_weight != WBQ_WEIGHT_IDENTITY) return WBQ_E_UNSUPPORTED;  // W1 = M: CPU oracle only (yet)
+    if (d.joint_weight != WBQ_WEIGHT_IDENTITY && d.joint_weight != WBQ_WEIGHT_INERTIA) return WBQ_E_INVALID;
     if (!d.Kc || !d.Dc || !d.Kq || !d.Dq || !d.tau_max || !d.tau_min) return WBQ_E_INVALID;
     int m0 = 0;
     int sel[wbq::kM0Max];
@@ -206,6 +206,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
                 sel[m0++] = t * 6 + r;
             }
     }
+    // W1 = M runs the active set in constraint space, one lane per level-0 row and torque limit
+    if (d.joint_weight == WBQ_WEIGHT_INERTIA && m0 + d.n > 64) return WBQ_E_UNSUPPORTED;
     wbq_ctx *c = new wbq_ctx();
     c->d = d;
     c->d.Kc = c->d.Dc = c->d.Kq = c->d.Dq = c->d.tau_max = c->d.tau_min = nullptr;
@@ -246,7 +248,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
          hipMemcpy(c->row_sel, sel, sizeof(int) * m0, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
     {
-        const size_t np = (size_t)wbq::lanes_per_instance(d.n);
+        // scratch lanes per instance (the W1 = M repair runs one instance per wave)
+        const size_t np = d.joint_weight == WBQ_WEIGHT_INERTIA ? 64 : (size_t)wbq::lanes_per_instance(d.n);
         ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
@@ -443,6 +446,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt)
     a.ntasks = c->d.ntasks;
     a.m0 = c->m0;
     a.select_mode = c->d.select_mode;
+    a.joint_weight = c->d.joint_weight;
     a.max_iter = c->d.max_iter;
     a.limits_crossed = c->limits_crossed;
     for (int t = 0; t < wbq::kTMax; ++t) a.row_mask[t] = t < c->d.ntasks ? c->d.row_mask[t] : 0;

@@ -15,6 +15,7 @@ struct QppvmArgs {
     int ntasks;      // Cartesian tasks
     int m0;          // level-0 rows (selected task rows)
     int select_mode; // WBQ_SELECT_*
+    int joint_weight; // WBQ_WEIGHT_*: W1 = I (qppvm_kernel.hip) or W1 = M (qppvm_w1m_kernel.hip)
     int max_iter;    // active-set step cap
     int limits_crossed; // some tau_min > tau_max (batch-shared limits): every instance infeasible
     int row_mask[kTMax];
@@ -59,6 +60,8 @@ constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
 // second launch follows (n > 32); n <= 32 is one launch (qppvm_single_launch).
 bool qppvm_single_launch(int n);
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
+// W1 = M (joint_weight 1): main kernel + level-0 repair kernel; needs m0 + n <= 64
+hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 
 // ------------------------------------------------------------------ contact form (ForceAcc)
 constexpr int kCMax = 4; // contacts

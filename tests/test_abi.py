@@ -94,3 +94,19 @@ def test_plugin_shells_export_factories():
         for sym in (f"create_instance_{cls}", f"destroy_instance_{cls}"):
             assert re.search(rf"\bT {sym}$", out, re.M), (lib, sym)
     assert os.access(driver, os.X_OK)
+
+
+def test_w1m_capacity_rejected_before_device(lib):
+    """W1 = M runs one lane per level-0 row and torque limit: m0 + n > 64 is refused (before
+    any device call, so this runs without a GPU); an unknown weight is invalid."""
+    import numpy as np
+    d = wbq.Desc()
+    d.form, d.n, d.ntasks, d.max_batch = wbq.FORM_QPPVM, 60, 2, 4
+    d.row_mask[0] = d.row_mask[1] = 0x3F  # m0 = 12
+    d.select_mode, d.joint_weight = 0, 1
+    keep = [np.ones(12), np.ones(12), np.ones(60), np.ones(60), np.full(60, 1.0), np.full(60, -1.0)]
+    d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [a.ctypes.data for a in keep]
+    h = ctypes.c_void_p()
+    assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_UNSUPPORTED
+    d.joint_weight = 2
+    assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_INVALID

@@ -37,8 +37,6 @@ def calibrated(prob_kw, n, inp, oracle_lib, frac):
 @pytest.mark.parametrize("n", [7, 30, 39])
 def test_golden_fixtures(wbq_mod, n):
     for g, prob, inp, exp in load_golden(n):
-        if prob.joint_weight != 0:
-            continue  # W1 = M: oracle-only (wbq_create returns WBQ_E_UNSUPPORTED)
         tau, st, it = gpu_solve(wbq_mod, prob, inp)
         # includes the level-0-infeasible groups (infeas0; the n = 7 groups with m0 > n),
         # which go through the in-kernel BVLS repair
