@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "batched WBC-QP solves/sec, ~30-DoF problem, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-DOMINANT = {"qppvm": "qppvm_fast_kernel", "contact": "contact_kernel"}
+DOMINANT = {"qppvm": "qppvm_fast_kernel", "contact": "contact_kernel", "qppvm_w1m": "qppvm_w1m_kernel"}
 TIMING_EVERY = 8  # HIP-event pairs around every 8th solve of the timed region
 HORIZON, MPC_DT = 20, 1e-3  # config 4: N = 20 sequential QPs per rollout, semi-implicit Euler
 
@@ -57,8 +57,8 @@ def contact_bytes(n, nc):
     return inputs + outputs
 
 
-def build_workload(form, config, n, B, world, rank, device):
-    """(problem, inputs, solver class) for this rank's shard."""
+def build_workload(form, config, n, B, world, rank, device, weight=0):
+    """(problem, inputs, solver class) for this rank's shard (weight: joint task W1 = I / M)."""
     from qppvm_amd.problem import ContactProblem, QPPVMProblem
     from qppvm_amd.shard import ShardPlan
     from qppvm_amd.synth import contact_instances, qppvm_instances, replicate
@@ -68,16 +68,17 @@ def build_workload(form, config, n, B, world, rank, device):
         config = 2  # MPC rollouts start from the config-2 random states
     if form == "qppvm":
         if config == 1:
-            prob = QPPVMProblem(n=n, tau_max=1e6)  # bounds inactive
+            prob = QPPVMProblem(n=n, tau_max=1e6, joint_weight=weight)  # bounds inactive
             return prob, replicate(qppvm_instances(prob, 1, seed=0), B), QPPVMSolver
         inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank))
         # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the first
         # B instances solved with the limits far away (same sample on every rank)
         calib = inp if rank == 0 else qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=0)
-        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B, device=device)
+        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9, joint_weight=weight), max_batch=B, device=device)
         tau_free, _, _ = free.solve_batch(calib)
         free.close()
-        return QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8))), inp, QPPVMSolver
+        return (QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)), joint_weight=weight), inp,
+                QPPVMSolver)
     if config == 1:  # double support, identical instances
         prob = ContactProblem(n=n, nc=2)
         return prob, replicate(contact_instances(prob, 1, seed=0), B), ContactSolver
@@ -92,10 +93,23 @@ def build_workload(form, config, n, B, world, rank, device):
     return prob, inp, ContactSolver
 
 
-def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False):
+def churn_pool(form, prob, n, B, world, rank):
+    """Second pool of random states for the config-2 churn (same distribution, seed 2)."""
+    from qppvm_amd.problem import ContactProblem, QPPVMProblem
+    from qppvm_amd.shard import ShardPlan
+    from qppvm_amd.synth import contact_instances, qppvm_instances
+    plan = ShardPlan(B * world, world)
+    if form == "qppvm":
+        return qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=2, offset=plan.start(rank))
+    return contact_instances(ContactProblem(n=n, nc=prob.nc), plan.count(rank), seed=2, offset=plan.start(rank),
+                             masks=[0b0011, 0b0111, 0b1111])
+
+
+def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False,
+        weight=0):
     """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
     import torch
-    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device)
+    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device, weight)
     solver = Solver(prob, max_batch=B, device=device)
     solver.set_inputs(inp)
     solver.sync()
@@ -106,6 +120,24 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         gather_buf = torch.empty((world * B, n), dtype=torch.float64, device="cuda")
         solver.set_stream(torch.cuda.current_stream().cuda_stream)
         solver.set_device_outputs(out.data_ptr())
+
+    churn = None
+    if config == 2:
+        # churn: every call re-randomises 20 % of the instances -- a
+        # rotating fifth of the rows is refreshed in HBM from a second pool of random states
+        # (seed 2; the pools alternate), warm-start state carried over. The inputs live in
+        # torch tensors adopted zero-copy; the refresh (a D2D copy of 20 % of the input
+        # bytes) runs on the solve stream inside the timed step.
+        pool = churn_pool(form, prob, n, B, world, rank)
+        keys = list(inp.keys())
+        dev = f"cuda:{device}"
+        live = {k: torch.from_numpy(np.ascontiguousarray(inp[k])).to(dev) for k in keys}
+        alt = [{k: live[k].clone() for k in keys},
+               {k: torch.from_numpy(np.ascontiguousarray(pool[k])).to(dev) for k in keys}]
+        solver.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        solver.set_device_inputs({k: live[k].data_ptr() for k in keys}, B)
+        churn = dict(live=live, alt=alt, calls=0, slice=(B + 4) // 5)
+        torch.cuda.synchronize()
 
     if config == 4:  # each MPC step re-plans from the measured state: a D2D reset of (q, qd)
         q0 = torch.from_numpy(np.ascontiguousarray(inp["q"])).to(f"cuda:{device}")
@@ -118,6 +150,13 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
             solver.solve()
             solver.outputs()
             return
+        if churn is not None:
+            c = churn["calls"]
+            lo = (c % 5) * churn["slice"]
+            src = churn["alt"][1 - (c // 5) % 2]  # pool states, then the originals, ...
+            for k, t in churn["live"].items():
+                t[lo:lo + churn["slice"]].copy_(src[k][lo:lo + churn["slice"]])
+            churn["calls"] = c + 1
         if config == 4:
             solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
             solver.rollout(HORIZON, MPC_DT)
@@ -162,6 +201,10 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
                 bytes_per_instance=per_inst, total=B * world * steps * qps)
 
 
+def dominant_kernel(form, weight):
+    return DOMINANT["qppvm_w1m"] if (form == "qppvm" and weight) else DOMINANT[form]
+
+
 def pmc_traffic(args, form):
     """Per-launch HBM bytes of the dominant kernel from two rocprofv3 PMC passes (one counter
     block each, kernel trace only), child processes of this not-yet-GPU-initialised process."""
@@ -169,13 +212,14 @@ def pmc_traffic(args, form):
     if prof is None:
         return None, "rocprofv3 not found"
     vals = {}
+    kern = dominant_kernel(form, 1 if args.weight == "M" else 0)
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             out = os.path.join(td, ctr)
             cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "run", "--",
                    sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-pmc", "--no-variant",
                    "--steps", "20", "--warmup", "2", "--form", form, "--config", str(args.config),
-                   "--batch", str(args.batch), "--n", str(args.n)]
+                   "--batch", str(args.batch), "--n", str(args.n), "--weight", args.weight]
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
@@ -187,10 +231,10 @@ def pmc_traffic(args, form):
             for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if DOMINANT[form] in row.get("Kernel_Name", ""):
+                        if kern in row.get("Kernel_Name", ""):
                             per.append(float(row["Counter_Value"]))
             if not per:
-                return None, f"{ctr}: no dispatches of {DOMINANT[form]}"
+                return None, f"{ctr}: no dispatches of {kern}"
             vals[ctr] = sum(per) / len(per)  # KB per dispatch
     fetch, write = vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
     return {"bytes": 2 * fetch + write, "fetch_raw": fetch, "write": write}, None
@@ -252,6 +296,7 @@ def main():
                     help="1: identical instances; 2: random states, bounds / contacts churn; "
                          "4: MPC, each step = HORIZON sequential solves per rollout (wbq_rollout)")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step")
+    ap.add_argument("--weight", choices=("I", "M"), default="I", help="QPPVM joint-task weight W1 (SURVEY 8a a6)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
@@ -275,15 +320,19 @@ def main():
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = local if dist else 0
     n, B = args.n, args.batch
+    weight = 1 if args.weight == "M" else 0
+    kern = dominant_kernel(args.form, weight)
     m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, args.allgather, dist,
-            args.host_io)
+            args.host_io, weight)
     value = m["total"] / m["dt"]
     bpl = m["bytes_per_instance"] * B
     achieved = bpl / (m["kavg_ms"] * 1e-3) / 1e9
     wl = {("qppvm", 1): "QPPVM 2-level torque QP, identical instances, bounds inactive (BASELINE config 1)",
-          ("qppvm", 2): "QPPVM 2-level torque QP, random states, ~20% torque bounds active (config 2)",
+          ("qppvm", 2): "QPPVM 2-level torque QP, random states, ~20% torque bounds active, 20% of the "
+                        "instances re-randomised per call (D2D refresh in the step), warm start carried (config 2)",
           ("contact", 1): "ForceAcc contact-form QP, double support (nc=2), identical instances (config 1 variant)",
-          ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows (config 2)",
+          ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows, 20% of the "
+                          "instances re-randomised per call (config 2)",
           ("qppvm", 4): f"MPC: rollouts x N={HORIZON} sequential QPPVM QPs, on-device semi-implicit Euler "
                         "(dt=1e-3), J/M/h frozen, warm-start carry (config 4)",
           ("contact", 4): f"MPC: rollouts x N={HORIZON} sequential contact-form QPs, on-device Euler (config 4)"}
@@ -301,13 +350,13 @@ def main():
         "dtype": "f64",
         "data": "synthetic randomized robot states (SURVEY 8d), " + (
             "host inputs/outputs over PCIe every step (--host-io)" if args.host_io else "inputs resident in HBM"),
-        "config": {"workload": f"{wl[(args.form, args.config)]}, n={n}, batch={B}/GPU",
+        "config": {"workload": f"{wl[(args.form, args.config)]}{', W1 = M' if weight else ''}, n={n}, batch={B}/GPU",
                    "global_batch": B * world, "n": n, "parallelism": f"shard{world}",
                    "allgather": bool(args.allgather)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic["bytes"],
-                     "kernel": DOMINANT[args.form], "kernel_avg_us": m["kavg_ms"] * 1e3,
+                     "kernel": kern, "kernel_avg_us": m["kavg_ms"] * 1e3,
                      "solve_avg_us": m["savg_ms"] * 1e3, "algorithmic_bytes_per_launch": bpl,
                      "algorithmic_bytes_per_instance": m["bytes_per_instance"],
                      "traffic_note": traffic_note if traffic is None else

@@ -141,6 +141,10 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
 // x = x0 + H^-1 A^T w with H^-1 A_q^T from the X^T slots and the diagonal force block.
 template <int NQ>
 struct ContactGi {
+    // Gamma mixes O(1) acceleration terms with O(1/eps_f) force terms: a force row's genuine
+    // complement can sit ~eps_f below its diagonal, so only roundoff-level ones count as
+    // dependent
+    static constexpr double kDep = 1e-14;
     double *S;
     const ContactLayout *L;
     int n, nf, i;

@@ -15,6 +15,7 @@
 //   double activity(int r) const          a_r . x at x = the current rebuilt x (LDS)
 //   void rebuild(int pass, int k) const   x = (pass 0: x0, else x) + H^-1 A^T w with the
 //                                          weights w in RV[0..k) on the rows AC[0..k)
+//   static constexpr double kDep          dependent-row threshold on Schur complement / Gamma_pp
 // and the LDS offsets of five 72-double scratch vectors (VV, LV, RV, WV, AC).
 #pragma once
 #include "wbq_device.h"
@@ -197,8 +198,7 @@ struct GAView {
     }
 };
 
-constexpr int kGiRounds = 8;      // x rebuilds (each followed by a re-check of every row)
-constexpr double kGiDep = 1e-10; // dependent-row threshold on the Schur complement / Gamma_pp
+constexpr int kGiRounds = 8; // x rebuilds (each followed by a re-check of every row)
 
 // LDS scratch vectors of the loop (72 doubles each: slot dots read 8 past the active count)
 struct GiVecs {
@@ -310,9 +310,9 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
         iargmin<64>(cand, blk);
         const double t1 = cand;
         // zz is the Schur complement of row cp against the active set, formed by cancellation:
-        // its roundoff is ~eps cond(Gamma_AA) gpp (1e-9 gpp at cond 1e7), so a row whose
-        // complement is below kGiDep gpp is dependent (no primal step), whatever its sign
-        const double t2 = (zz > kGiDep * gpp) ? -slack / zz : kInf;
+        // its roundoff is ~eps cond(Gamma_AA) gpp, so a row whose complement is below
+        // P::kDep gpp is dependent (no primal step), whatever its sign
+        const double t2 = (zz > P::kDep * gpp) ? -slack / zz : kInf;
         if (t1 >= kInf && t2 >= kInf) {
             g.status = 2; // no step: the rows cannot all be met
             break;

@@ -75,6 +75,10 @@ struct RepairIn {
 };
 
 struct W1mGi {
+    // Gamma = [G M^-1 G^T, G; G^T, M] is well scaled, but degenerate active sets (level-0 rows
+    // plus pinned limits) push cond(Gamma_AA) to ~1e7: complements below 1e-10 Gamma_pp are
+    // roundoff (scripts/emulate_w1m.py)
+    static constexpr double kDep = 1e-10;
     double *S;
     const W1mLayout *L;
     int m0, n, i;
