@@ -149,6 +149,7 @@ struct ContactGi {
     const ContactLayout *L;
     int n, nf, i;
     double ieps;
+    int dim; // n + nf
     __device__ double gamma(int r, int c) const { return S[L->GM + r * L->GS + c]; }
     __device__ double activity(int r) const { return wbq::activity<NQ>(S, *L, r, n, nf); }
     __device__ void rebuild(int pass, int k) const
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         __syncthreads();
     }
     {
-        const ContactGi<NQ> pb{S, &L, n, nf, i, ieps};
+        const ContactGi<NQ> pb{S, &L, n, nf, i, ieps, L.NX};
         dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }

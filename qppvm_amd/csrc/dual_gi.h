@@ -16,6 +16,7 @@
 //   void rebuild(int pass, int k) const   x = (pass 0: x0, else x) + H^-1 A^T w with the
 //                                          weights w in RV[0..k) on the rows AC[0..k)
 //   static constexpr double kDep          dependent-row threshold on Schur complement / Gamma_pp
+//   int dim                               primal dimension (at most dim independent rows)
 // and the LDS offsets of five 72-double scratch vectors (VV, LV, RV, WV, AC).
 #pragma once
 #include "wbq_device.h"
@@ -217,7 +218,7 @@ struct GiState {
 // The loop itself (lane i = constraint row i; kind 0 disabled, 1 equality already in the
 // active set, 2 a row with limits [lo, hi], lo == hi an equality added when violated).
 // Statuses: 1 step cap, 2 no step exists (the rows are inconsistent: infeasible), 3 the slot
-// storage overflowed (dependent rows). On exit with status 0, x in LDS and s_i are exact.
+// storage overflowed or the rebuilt x misses an active row (a numerically dependent set). On exit with status 0, x in LDS and s_i are exact.
 template <int KM, class P, class TrowT, class TcolT, class GAT>
 __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V, int i, TrowT &Trow, TcolT &Tcol,
                                         GAT &GA, int kind, double lo, double hi, double nrm, double &s_i, GiState &g,
@@ -274,6 +275,13 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                     __syncthreads();
                 }
                 if (kind != 0) s_i = pb.activity(i);
+                // the active rows must hold at the rebuilt x; if one does not, T (the factor
+                // of a nearly dependent active set) is garbage and so is x: fail loudly
+                const double miss = (kind != 0 && g.onact) ? fmin(fabs(s_i - lo), fabs(s_i - hi)) / (1.0 + fabs(s_i)) : 0.0;
+                if (imax<64>(miss) > 1e-8) {
+                    g.status = 3;
+                    break;
+                }
                 continue;
             }
             cp = pi;
@@ -312,7 +320,8 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
         // zz is the Schur complement of row cp against the active set, formed by cancellation:
         // its roundoff is ~eps cond(Gamma_AA) gpp, so a row whose complement is below
         // P::kDep gpp is dependent (no primal step), whatever its sign
-        const double t2 = (zz > P::kDep * gpp) ? -slack / zz : kInf;
+        // and with k = dim active rows the set spans the primal space: cp is dependent
+        const double t2 = (g.k < pb.dim && zz > P::kDep * gpp) ? -slack / zz : kInf;
         if (t1 >= kInf && t2 >= kInf) {
             g.status = 2; // no step: the rows cannot all be met
             break;

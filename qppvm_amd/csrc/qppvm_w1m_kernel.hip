@@ -82,6 +82,7 @@ struct W1mGi {
     double *S;
     const W1mLayout *L;
     int m0, n, i;
+    int dim; // n
     __device__ double gamma(int r, int c) const { return S[L->GM + r * L->GS + c]; }
     __device__ double activity(int r) const
     {
@@ -292,14 +293,16 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     gs.status = st0 != 0 ? st0 : (notspd ? 3 : (a.limits_crossed ? 2 : 0));
     __syncthreads();
     {
-        const W1mGi pb{S, &L, m0, n, i};
+        const W1mGi pb{S, &L, m0, n, i, n};
         dual_gi<64>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }
     __syncthreads();
     int status = gs.status;
-    if (status == 2 && !R && !a.limits_crossed && !notspd) {
-        // no step: level 0 is not attainable at b0 inside the limits -> repair kernel (y*)
+    if ((status == 2 || status == 3) && !R && !a.limits_crossed && !notspd) {
+        // no step: level 0 is not attainable at b0 inside the limits; or the active set went
+        // numerically dependent, which near-inconsistent level-0 rows also cause -> repair
+        // kernel (y* and the pins make the level-1 rows consistent)
         if (i < 64) a.ui_scr[b * 64 + i] = S[L.U0 + i];
         if (i < m0) a.b0_scr[b * kM0Max + i] = b0;
         if (i == 0) {

@@ -1,0 +1,94 @@
+"""KAT-4: optimality certificates for a solver output, computed from the
+assembled problem alone -- no reference solution, so they hold at any batch size.
+
+QPPVM (oracle/wbq_oracle.c:wbq_ref_assemble: A0 = G M^-1, b0, lb, ub; x = tau - h):
+  level 0   x is a minimiser of 0.5 ||A0 x - b0||^2 over the box: with the gradient
+            g0 = A0^T (A0 x - b0), g0_j = 0 where x_j is free, >= 0 at lb, <= 0 at ub;
+  level 1   x minimises the joint task over {A0 x = A0 x, box}: M grad f1 = G^T nu + M mu
+            (M grad f1 = M^-1 (x - tau_imp) for W1 = I, x - tau_imp for W1 = M), mu_j >= 0
+            at lb, <= 0 at ub, 0 where free; variables level 0 pins (|g0_j| above roundoff)
+            are fixed for level 1 and carry a multiplier of either sign;
+  primal    lb <= x <= ub.
+Contact form (oracle/wbq_oracle_contact.c:wbq_ref_contact_assemble: H, g, E x = e, clo <= C x
+<= chi): H x + g = E^T nu + C^T mu with mu >= 0 on rows at clo, <= 0 at chi, and primal
+feasibility. Residuals are scaled; the multipliers of a rank-deficient active set are not
+unique, so their signs are checked only where the active normals are independent.
+"""
+import numpy as np
+
+
+def _tau_imp(prob, inp, b):
+    return prob.Kq * (inp["qref"][b] - inp["q"][b]) - prob.Dq * inp["qd"][b]
+
+
+def _active(v, lo, hi, tol):
+    at_lo = v - lo <= tol * (1.0 + np.abs(lo))
+    at_hi = hi - v <= tol * (1.0 + np.abs(hi))
+    return at_lo, at_hi
+
+
+def qppvm_certificate(oracle, prob, inp, b, tau):
+    """Scaled residuals of instance b's output tau: dict(primal, level0, stat, sign, indep)."""
+    M = inp["M"][b]
+    a = oracle.assemble(prob, inp, b)
+    A0, b0, lb, ub = a["A0"], a["b0"], a["lb"], a["ub"]
+    x = tau - inp["h"][b]
+    scale = 1.0 + np.abs(np.concatenate([lb, ub])).max()
+    primal = max(0.0, (lb - x).max(), (x - ub).max()) / scale
+    at_lo, at_hi = _active(x, lb, ub, 1e-9)
+    free = ~(at_lo | at_hi)
+    g0 = A0.T @ (A0 @ x - b0)
+    s0 = np.abs(A0.T).sum(axis=1) * (np.abs(A0 @ x).max() + np.abs(b0).max()) + 1e-300
+    l0 = np.where(free, np.abs(g0), 0.0)
+    l0 = np.maximum(l0, np.where(at_lo & ~at_hi, np.maximum(-g0, 0.0), 0.0))
+    l0 = np.maximum(l0, np.where(at_hi & ~at_lo, np.maximum(g0, 0.0), 0.0))
+    level0 = float((l0 / s0).max())
+    pinned = np.abs(g0) > 1e-7 * s0  # level 0 holds these at their bound
+    G = A0 @ M
+    timp = _tau_imp(prob, inp, b)
+    r = np.linalg.solve(M, x - timp) if prob.joint_weight == 0 else x - timp
+    act = np.where(~free)[0]
+    K = np.concatenate([G.T, M[:, act]], axis=1)
+    lam, *_ = np.linalg.lstsq(K, r, rcond=None)
+    stat = float(np.abs(r - K @ lam).max() / (np.abs(r).max() + np.abs(K @ lam).max() + 1e-300))
+    mu = lam[G.shape[0]:]
+    indep = np.linalg.matrix_rank(K, tol=1e-10 * np.abs(K).max()) == K.shape[1]
+    sign = 0.0
+    if indep:
+        mscale = np.abs(lam).max() + 1e-300
+        for c, j in enumerate(act):
+            if pinned[j] or lb[j] == ub[j]:
+                continue
+            if at_lo[j] and not at_hi[j]:
+                sign = max(sign, -mu[c] / mscale)
+            elif at_hi[j] and not at_lo[j]:
+                sign = max(sign, mu[c] / mscale)
+    return dict(primal=primal, level0=level0, stat=stat, sign=sign, indep=bool(indep))
+
+
+def contact_certificate(oracle, prob, inp, b, x):
+    """Scaled residuals of instance b's contact-form output x = [qdd; f]."""
+    a = oracle.contact_assemble(prob, inp, b)
+    H, g, E, e, C, clo, chi = a["H"], a["g"], a["E"], a["e"], a["C"], a["clo"], a["chi"]
+    cx = C @ x
+    scale = 1.0 + max(np.abs(e).max(), np.abs(np.concatenate([clo, chi])[np.isfinite(np.concatenate([clo, chi]))]).max(initial=0.0))
+    primal = max(np.abs(E @ x - e).max(), max(0.0, (clo - cx).max(initial=0.0), (cx - chi).max(initial=0.0))) / scale
+    at_lo, at_hi = _active(cx, clo, chi, 1e-9)
+    act = np.where(at_lo | at_hi)[0]
+    K = np.concatenate([E.T, C[act].T], axis=1)
+    r = H @ x + g
+    lam, *_ = np.linalg.lstsq(K, r, rcond=None)
+    stat = float(np.abs(r - K @ lam).max() / (np.abs(H @ x).max() + np.abs(g).max() + 1e-300))
+    indep = np.linalg.matrix_rank(K, tol=1e-10 * np.abs(K).max()) == K.shape[1]
+    sign = 0.0
+    if indep:
+        mu = lam[E.shape[0]:]
+        mscale = np.abs(lam).max() + 1e-300
+        for c, j in enumerate(act):
+            if clo[j] == chi[j]:
+                continue
+            if at_lo[j] and not at_hi[j]:
+                sign = max(sign, -mu[c] / mscale)
+            elif at_hi[j] and not at_lo[j]:
+                sign = max(sign, mu[c] / mscale)
+    return dict(primal=primal, stat=stat, sign=sign, indep=bool(indep))

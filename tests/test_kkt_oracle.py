@@ -1,0 +1,44 @@
+"""The KAT-4 optimality certificates (tests/kkt.py) themselves, on CPU: the oracle's solutions
+pass them; perturbed solutions and the solution of the other joint weight fail them."""
+import numpy as np
+import pytest
+
+import kkt
+from qppvm_amd.problem import ContactProblem, QPPVMProblem, WEIGHT_IDENTITY, WEIGHT_INERTIA
+from qppvm_amd.synth import contact_instances, qppvm_instances
+
+TOL = 1e-9
+
+
+def worst(cs, keys):
+    return {k: max(c[k] for c in cs) for k in keys}
+
+
+@pytest.mark.parametrize("weight", [WEIGHT_IDENTITY, WEIGHT_INERTIA])
+def test_qppvm_certificate_accepts_oracle_and_rejects_others(oracle_lib, weight):
+    free = QPPVMProblem(n=30, tau_max=1e9, joint_weight=weight)
+    inp = qppvm_instances(free, 24, seed=11)
+    t0, _, _ = oracle_lib.qppvm_batch(free, inp)
+    prob = QPPVMProblem(n=30, tau_max=float(np.quantile(np.abs(t0), 0.8)), joint_weight=weight)
+    tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
+    assert (st == 0).all()
+    ok = worst([kkt.qppvm_certificate(oracle_lib, prob, inp, b, tau[b]) for b in range(24)],
+               ("primal", "level0", "stat", "sign"))
+    assert max(ok.values()) <= TOL, ok
+    bad = [kkt.qppvm_certificate(oracle_lib, prob, inp, b, tau[b] * (1 + 1e-6)) for b in range(8)]
+    assert all(max(c["primal"], c["level0"], c["stat"]) > 1e-8 for c in bad)
+    other = QPPVMProblem(n=30, tau_max=prob.tau_max, joint_weight=1 - weight)
+    tau_o, st_o, _ = oracle_lib.qppvm_batch(other, inp)
+    wrong = [kkt.qppvm_certificate(oracle_lib, prob, inp, b, tau_o[b]) for b in range(24) if st_o[b] == 0]
+    assert sum(c["stat"] > 1e-6 for c in wrong) >= len(wrong) // 2
+
+
+def test_contact_certificate_accepts_oracle_and_rejects_perturbed(oracle_lib):
+    prob = ContactProblem(n=30, nc=4)
+    inp = contact_instances(prob, 16, seed=12, masks=[0b0011, 0b0111, 0b1111])
+    _, x, st, _, _ = oracle_lib.contact_batch(prob, inp)
+    ok = worst([kkt.contact_certificate(oracle_lib, prob, inp, b, x[b]) for b in range(16) if st[b] == 0],
+               ("primal", "stat", "sign"))
+    assert max(ok.values()) <= TOL, ok
+    bad = [kkt.contact_certificate(oracle_lib, prob, inp, b, x[b] * (1 + 1e-6)) for b in range(8)]
+    assert all(max(c["primal"], c["stat"]) > 1e-9 for c in bad)
