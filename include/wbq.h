@@ -75,7 +75,11 @@ extern "C" {
 #define WBQ_SELECT_SUBTASK 0 /* full 6-D task built, rows selected afterwards */
 #define WBQ_SELECT_TASK 1    /* task-space force masked before J^T F */
 
-/* joint-task weight on level 1 */
+/* joint-task weight W1 on level 1 (JointImpedanceCtrl, QPPVMPlugin.cpp:114-118):
+ * IDENTITY  min ||M^-1 (x - tau_imp)||^2      (KAT-1)
+ * INERTIA   min (x - tau_imp)^T M^-1 (x - tau_imp), the dynamically consistent form (KAT-2);
+ *           needs m0 + n <= 64 (one lane per level-0 row and torque limit), else
+ *           wbq_create returns WBQ_E_UNSUPPORTED */
 #define WBQ_WEIGHT_IDENTITY 0
 #define WBQ_WEIGHT_INERTIA 1
 
