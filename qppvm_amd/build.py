@@ -23,15 +23,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
-    """diag=True builds libwbq_diag.so with in-kernel phase stamps (never the product)."""
-    lib = LIB.replace("libwbq.so", "libwbq_diag.so") if diag else LIB
-    if not force and not diag and not _stale():
+def build(force: bool = False, verbose: bool = False, diag: bool = False, defines: tuple = (),
+          out: str | None = None) -> str:
+    """diag=True builds libwbq_diag.so with in-kernel phase stamps (never the product);
+    defines/out build an experiment variant (scripts/ab_bench.py) at another path."""
+    lib = out or (LIB.replace("libwbq.so", "libwbq_diag.so") if diag else LIB)
+    if not force and not diag and out is None and not _stale():
         return LIB
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
            "-I", os.path.join(ROOT, "include"),
-           *(["-DWBQ_STAMPS"] if diag else []),
+           *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines],
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

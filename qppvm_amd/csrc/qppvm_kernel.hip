@@ -428,6 +428,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const int voff = (int)(8 * (bn + ic));
     const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
     const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    // the warm-start hint is issued before the bulk loads: vmcnt retires in order, so a load
+    // issued after M and waited for early would drain all of M with it
+    const unsigned char hint_b = a.ws_hint[valid ? b : 0]; // unconditional: no branch on it here
     // J and the poses first, M last: vmcnt waits are in order, so the task forces (J, poses,
     // qd) can start while M is still streaming in
     double jv[kTMax * 6];
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 #pragma unroll
     for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     const double h_i = row ? h_i0 : 0.0;
-    const bool hint = valid && a.ws_hint[b] != 0; // the last solve needed the level-0 repair
+    const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
 #pragma unroll
     for (int rr = 0; rr < kTMax * 6; ++rr)
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 #pragma unroll
     for (int it = 0; it < kPoseIt; ++it)
         if (it * NP + i < T * 24) S[L.PS + it * NP + i] = valid ? pv[it] : 0.0;
-    __syncthreads();
+    lds_barrier(); // M keeps streaming in behind the forces
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
         const int t = i / 6, r = i - t * 6;

@@ -292,6 +292,69 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     GiState gs;
     gs.status = st0 != 0 ? st0 : (notspd ? 3 : (a.limits_crossed ? 2 : 0));
     __syncthreads();
+    if (gs.status == 0) {
+        // The m0 level-0 rows in one batch when Gamma_EE is well conditioned (dependent rows
+        // are left to the loop, which never adds them): lane r < m0 holds row r of Gamma_EE, a
+        // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane c
+        // forward-substitutes column c of T = L^-1, and lambda_E = T^T T (b0 - s_E).
+        double g[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) g[c] = (i < m0 && c < m0) ? S[L.GM + i * L.GS + c] : 0.0;
+        double gd = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) gd = (i == c) ? g[c] : gd;
+        const double dmx = imax<64>(gd);
+        bool sing = false;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            if (c < m0) {
+                const double dcc = bcast(g[c], c);
+                sing |= !(dcc > 1e-10 * dmx);
+                const double ilc = dcc > 0.0 ? frsq(dcc) : 0.0;
+                g[c] = (i > c) ? g[c] * ilc : ((i == c) ? dcc * ilc : g[c]); // L[r][c], r >= c
+#pragma unroll
+                for (int j = c + 1; j < M0; ++j) {
+                    if (j < m0) {
+                        const double ljc = bcast(g[c], j);
+                        if (i >= j) g[j] = fma(-g[c], ljc, g[j]);
+                    }
+                }
+            }
+        }
+        if (!sing) {
+            double t[M0]; // column i of T (lanes i < m0)
+#pragma unroll
+            for (int r = 0; r < M0; ++r) {
+                double acc = (i == r) ? 1.0 : 0.0;
+#pragma unroll
+                for (int q = 0; q < r; ++q) acc = fma(-bcast(g[q], r < m0 ? r : 0), t[q], acc);
+                const double lrr = r < m0 ? bcast(g[r], r) : 0.0;
+                t[r] = (i < m0 && lrr > 0.0) ? acc / lrr : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < M0; ++r)
+                if (r < m0 && i < m0) S[L.TT + r * L.TS + i] = t[r]; // T rows (lane c writes column c)
+            if (i < m0) S[L.VV + i] = lo - s_i;                       // b0 - s_E
+            S[L.AC + i] = (double)i;                                   // slot q = row q
+            __syncthreads();
+            const double w = i < m0 ? Trow.dot(S + L.VV, m0) : 0.0;
+            S[L.LV + i] = w;
+            __syncthreads();
+            const double lm = i < m0 ? Tcol.dot(S + L.LV, m0) : 0.0; // lambda_E
+            S[L.RV + i] = lm;
+            __syncthreads();
+            if (kind != 0) s_i += GA.dot(S + L.RV, m0);
+            if (i < m0) {
+                gs.act = i;
+                gs.aeq = true;
+                gs.lam = lm;
+                gs.onact = true;
+            }
+            gs.k = m0;
+            gs.iters = 1;
+            __syncthreads();
+        }
+    }
     {
         const W1mGi pb{S, &L, m0, n, i, n};
         dual_gi<64>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,

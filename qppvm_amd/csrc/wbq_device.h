@@ -21,6 +21,21 @@ constexpr double kInf = 1.0e300;
 #define WBQ_STAMP(k) do {} while (0)
 #endif
 
+// Workgroup barrier that orders LDS only. __syncthreads() is a workgroup fence on every
+// address space, so it drains this wave's outstanding global loads (vmcnt(0)) before the
+// barrier; with the fence narrowed to LDS ("local") the barrier waits for lgkmcnt only and
+// loads issued before it stay in flight (the stage's M rows stream in behind the forces).
+__device__ __forceinline__ void lds_barrier()
+{
+#ifdef WBQ_AB_FULL_BARRIER
+    __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
+}
+
 // fast reciprocal / reciprocal square root: hardware estimate + one Newton step (~0.5 ulp)
 __device__ __forceinline__ double frcp(double x)
 {
