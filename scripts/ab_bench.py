@@ -7,6 +7,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import torch  # noqa: E402  (torch's HIP runtime first, as in bench.py)
+
+torch.cuda.init()
 from qppvm_amd import wbq  # noqa: E402
 
 wbq.load_library(os.path.abspath(sys.argv[1]))  # cached: every solver in bench.py uses it
