@@ -62,22 +62,44 @@ struct ContactLayout {
         GS = ME | 1;
         TS = (NX + 8) | 1;    // the active set never exceeds NX independent rows (+8: chunked dots)
         int o = 0;
-        AQJ = o; o += NJ * QS;    // joint constraint rows, acceleration part: M row a
-        AQW = o; o += 6 * QS;     // waist rows: J_w row r
+        if (!tr) {
+            AQJ = o; o += NJ * QS;    // joint constraint rows, acceleration part: M row a
+            AQW = o; o += 6 * QS;     // waist rows: J_w row r
+        }
         FFJ = o; o += NJ * FS;    // their force part: -J_c[0:3, a] (active contacts)
         XT = o; o += NR * QS;     // X^T: slot s = column s of H^-1 A_q^T over the qdd lanes
         GM = o; o += ME * GS;     // Gamma
         TT = o;                   // T = L^-1 of the active-set Gram, rows of TS
-        // setup-phase overlays of the TT region. The contact Jacobian rows are dead once H is
-        // assembled (a barrier precedes the elimination), so the Gauss-Jordan panel reuses them:
-        // 22 KB -> 19.6 KB per instance at n = 30, nc = 2, i.e. 8 instances per CU instead of 7
-        const int jcs = 6 * nc * NQ, gjs = 2 * NQ * 4 + 2 * 4 * NRC;
-        int ov = jcs > gjs ? jcs : gjs;
-        JC = TT;                  // contact Jacobian rows (steps 1-3)
-        PN = TT;                  // Gauss-Jordan pivot panel (rows < NQ publish; step 4)
-        RH = TT + 2 * NQ * 4;     // its right-hand sides
-        HR = TT + ov; ov += (NQ == 64 && tr) ? NQ * QS : 0; // H rows for a second rhs chunk
-                                  // (written before that barrier: not over JC)
+        int ov = 0;               // setup-phase overlays of the TT region
+        if (tr) {
+            // Torque-row form (LDS-bound occupancy): everything the dual loop does not read lives
+            // in the TT region, which the loop only writes after Gamma is assembled. A_q rows
+            // (each lane keeps its own row in registers for the loop's activities), task data,
+            // the Gauss-Jordan panel; the contact Jacobian rows (dead before the elimination
+            // writes X^T) in the X^T region. 64.8 -> 53.3 KB at n = 30, nc = 4: 3 instances per
+            // CU instead of 2.
+            AQJ = TT + ov; ov += NJ * QS;
+            AQW = TT + ov; ov += 6 * QS;
+            QD = TT + ov; ov += 64;
+            PS = TT + ov; ov += 24 * (1 + nc);
+            BT = TT + ov; ov += 6 * (1 + nc);
+            JD = TT + ov; ov += 6 * (1 + nc);
+            const bool jc_in_xt = 6 * nc * NQ <= NR * QS;
+            JC = jc_in_xt ? XT : TT + ov; ov += jc_in_xt ? 0 : 6 * nc * NQ;
+            PN = TT + ov; ov += 2 * NQ * 4;   // Gauss-Jordan pivot panel (rows < NQ publish)
+            RH = TT + ov; ov += 2 * 4 * NRC;  // its right-hand sides
+            HR = TT + ov; ov += NQ == 64 ? NQ * QS : 0; // H rows for a second rhs chunk
+        } else {
+            // The contact Jacobian rows are dead once H is assembled (a barrier precedes the
+            // elimination), so the Gauss-Jordan panel reuses them: 22 KB -> 19.6 KB per instance
+            // at n = 30, nc = 2, i.e. 8 instances per CU instead of 7
+            const int jcs = 6 * nc * NQ, gjs = 2 * NQ * 4 + 2 * 4 * NRC;
+            ov = jcs > gjs ? jcs : gjs;
+            JC = TT;                  // contact Jacobian rows (steps 1-3)
+            PN = TT;                  // Gauss-Jordan pivot panel (rows < NQ publish; step 4)
+            RH = TT + 2 * NQ * 4;     // its right-hand sides
+            HR = TT;                  // (unused: NQ == 64 && tr only)
+        }
         // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns
         const int tt = tr ? NX * TS : 12 * TS; // (!tr: scratch for the T_E rows)
         o += tt > ov ? tt : ov;
@@ -89,10 +111,12 @@ struct ContactLayout {
         WV = o; o += 72;
         DUM = o; o += 72;         // row of the lanes that own no slot-vector row
         AC = o; o += 72;          // active constraint (compact index) per slot (+8: chunked gathers)
-        PS = o; o += 24 * (1 + nc);      // poses: waist, then contacts ([R|p], ref)
-        BT = o; o += 6 * (1 + nc);       // task targets: waist b_w, then b_c
-        JD = o; o += 6 * (1 + nc);       // Jdot qd
-        QD = o; o += 64;
+        if (!tr) {
+            PS = o; o += 24 * (1 + nc);      // poses: waist, then contacts ([R|p], ref)
+            BT = o; o += 6 * (1 + nc);       // task targets: waist b_w, then b_c
+            JD = o; o += 6 * (1 + nc);       // Jdot qd
+            QD = o; o += 64;
+        }
         SIZE = (o + 1) & ~1;
     }
 };
@@ -144,7 +168,7 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
 
 // The contact problem for dual_gi: Gamma in LDS, activities from the rows in LDS, and
 // x = x0 + H^-1 A^T w with H^-1 A_q^T from the X^T slots and the diagonal force block.
-template <int NQ>
+template <int NQ, bool TR>
 struct ContactGi {
     // Gamma mixes O(1) acceleration terms with O(1/eps_f) force terms: a force row's genuine
     // complement can sit ~eps_f below its diagonal, so only roundoff-level ones count as
@@ -155,8 +179,30 @@ struct ContactGi {
     int n, nf, i;
     double ieps;
     int dim; // n + nf
+    double aq[TR ? NQ : 1]; // TR: this lane's own A_q row (the LDS rows are overlaid by T)
     __device__ double gamma(int r, int c) const { return S[L->GM + r * L->GS + c]; }
-    __device__ double activity(int r) const { return wbq::activity<NQ>(S, *L, r, n, nf); }
+    __device__ double activity(int r) const
+    {
+        if constexpr (!TR) {
+            return wbq::activity<NQ>(S, *L, r, n, nf);
+        } else { // r == this lane's row (dual_gi asks for its own row only)
+            const double *xv = S + L->XV;
+            const bool jrow = r < L->NJ, wrow = !jrow && r < L->NJ + 6;
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < NQ; j += 2) {
+                s0 = fma(aq[j], xv[j], s0);
+                s1 = fma(aq[j + 1], xv[j + 1], s1);
+            }
+            const double *fr = S + L->FFJ + (jrow ? r : 0) * L->FS;
+            double sf = 0.0;
+#pragma unroll
+            for (int f = 0; f < 3 * kCMax; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
+            if (jrow) return (s0 + s1) + sf;
+            if (wrow) return s0 + s1;
+            return xv[n + r - L->NJ - 6];
+        }
+    }
     __device__ void rebuild(int pass, int k) const
     {
         if (i >= L->NX) return;
@@ -361,8 +407,11 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     }
     const double ieps = 1.0 / a.eps_f;
     double s_i = 0.0, nrm = 1.0;
+    double aq[NQ]; // this lane's acceleration row (kept in registers for the TR loop)
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) aq[j] = 0.0;
     if (kind != 0) {
-        double aq[NQ], fc[3 * kCMax];
+        double fc[3 * kCMax];
         const double *rq = row_q(S, L, ci);
 #pragma unroll
         for (int j = 0; j < NQ; ++j) aq[j] = rq ? rq[j] : 0.0;
@@ -487,7 +536,11 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         __syncthreads();
     }
     {
-        const ContactGi<NQ> pb{S, &L, n, nf, i, ieps, L.NX};
+        ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, L.NX};
+        if constexpr (TR) {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
+        }
         dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }
