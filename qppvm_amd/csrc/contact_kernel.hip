@@ -174,6 +174,7 @@ struct ContactGi {
     // complement can sit ~eps_f below its diagonal, so only roundoff-level ones count as
     // dependent
     static constexpr double kDep = 1e-14;
+    static constexpr bool kOwnRowActivity = TR;
     double *S;
     const ContactLayout *L;
     int n, nf, i;

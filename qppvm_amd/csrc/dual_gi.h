@@ -12,8 +12,9 @@
 //
 // The problem supplies a policy P with
 //   double gamma(int r, int c) const      Gamma[r][c]
-//   double activity(int r) const          a_r . x at x = the current rebuilt x (LDS); called
-//                                         with the lane's own row only (r == lane, or 0 on no-row lanes)
+//   double activity(int r) const          a_r . x at x = the current rebuilt x (LDS)
+//   static bool kOwnRowActivity           activity(r) only for the lane's own row (r == lane, or 0
+//                                         on no-row lanes): its row lives in registers
 //   void rebuild(int pass, int k) const   x = (pass 0: x0, else x) + H^-1 A^T w with the
 //                                          weights w in RV[0..k) on the rows AC[0..k)
 //   static constexpr double kDep          dependent-row threshold on Schur complement / Gamma_pp
@@ -260,9 +261,13 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 for (int pass = 0; pass < 3; ++pass) {
                     if (pass > 0) {
                         // residual of the active rows, exact in x-space; correction through T
-                        // every lane evaluates its own row, slot lanes pick their active row's
-                        const double a_own = pb.activity(kind != 0 ? i : 0);
-                        const double a_act = __shfl(a_own, g.act);
+                        double a_act;
+                        if constexpr (P::kOwnRowActivity) { // every lane its own row, slots gather
+                            const double a_own = pb.activity(kind != 0 ? i : 0);
+                            a_act = __shfl(a_own, g.act);
+                        } else {
+                            a_act = i < g.k ? pb.activity(g.act) : 0.0;
+                        }
                         const double res = i < g.k ? g.sgn * ((g.sgn > 0.0 ? lo_a : hi_a) - a_act) : 0.0;
                         S[V.VV + i] = res;
                         __syncthreads();

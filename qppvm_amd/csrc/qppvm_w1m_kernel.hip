@@ -33,38 +33,44 @@ namespace {
 //   ci < m0              level-0 row c = ci:  (G M^-1)_c x = b0_c (y*_c after the repair)
 //   m0 <= ci < m0 + n    torque limit of joint j = ci - m0:  lo_j <= x_j <= hi_j
 struct W1mLayout {
-    int ME, QS, GS, TS;
+    int ME, QS, GS, TS, KT;
     int JR, XG, GM, TT, PN, RH, XV, X0, U0, WT, VV, LV, RV, WV, DUM, AC, PS, F, QD, SIZE;
     __host__ __device__ W1mLayout(int n, int T, int m0, int NQ, int NRC)
     {
         ME = m0 + n;
         QS = NQ + 1;
         GS = ME | 1;
-        TS = (ME + 8) | 1;
+        KT = n > m0 ? n : m0;      // T rows: the active set never exceeds the primal dimension n
+                                   // (dual_gi's cap), the level-0 batch writes m0 rows
+        TS = (KT + 8) | 1;
         int o = 0;
-        JR = o; o += T * 6 * NQ;   // J rows
-        XG = o; o += kM0Max * QS;  // row c = (M^-1 G^T)[:, c] over the joint lanes
-        GM = o; o += ME * GS;      // Gamma; its columns >= m0 are the rows of A M = (H^-1 A^T)^T
+        XG = o; o += (m0 * QS + 1) & ~1; // row c = (M^-1 G^T)[:, c] over the joint lanes
+        GM = o; o += (ME * GS + 1) & ~1; // Gamma; its columns >= m0 are the rows of A M = (H^-1 A^T)^T
         TT = o;                    // T = L^-1 of the active-set Gram (rows of TS)
-        PN = TT;                   // Gauss-Jordan pivot panel / rhs (setup overlay of TT)
-        RH = PN + 2 * NQ * 4;
         {
-            const int tt = ME * TS, ov = 2 * NQ * 4 + 2 * 4 * NRC;
+            // setup-only data overlays T (first written after the barrier that ends the Gamma
+            // assembly): J rows, task data, J_t^T F_t and the Gauss-Jordan panel. With KT rows
+            // this is 36.9 -> 26.6 KB per instance at n = 30: 6 instances per CU instead of 4
+            int ov = 0;
+            JR = TT + ov; ov += T * 6 * NQ;     // J rows
+            WT = TT + ov; ov += T * NQ;         // J_t^T F_t
+            PS = TT + ov; ov += 24 * T;         // poses [R|p], ref
+            F = TT + ov; ov += (6 * T + 1) & ~1; // task forces
+            QD = TT + ov; ov += 64;
+            PN = TT + ov; ov += 2 * NQ * 4;     // Gauss-Jordan pivot panel
+            RH = TT + ov; ov += 2 * 4 * NRC;    // its right-hand sides
+            const int tt = KT * TS;
             o += tt > ov ? tt : ov;
         }
         XV = o; o += 64;           // x
         X0 = o; o += 64;           // x0 = tau_imp
         U0 = o; o += 64;           // u_imp = M^-1 tau_imp
-        WT = o; o += kTMax * NQ;   // J_t^T F_t
         VV = o; o += 72;
         LV = o; o += 72;
         RV = o; o += 72;
         WV = o; o += 72;
         DUM = o; o += 72;          // row of the lanes that own no T row
         AC = o; o += 72;
-        PS = o; o += 24 * T;       // poses [R|p], ref
-        F = o; o += 6 * T;         // task forces
-        QD = o; o += 64;
         SIZE = (o + 1) & ~1;
     }
 };
@@ -75,6 +81,7 @@ struct RepairIn {
 };
 
 struct W1mGi {
+    static constexpr bool kOwnRowActivity = false;
     // Gamma = [G M^-1 G^T, G; G^T, M] is well scaled, but degenerate active sets (level-0 rows
     // plus pinned limits) push cond(Gamma_AA) to ~1e7: complements below 1e-10 Gamma_pp are
     // roundoff (scripts/emulate_w1m.py)
@@ -284,8 +291,8 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     SlotVec<64, false> Trow;
     TColView Tcol;
     GAView GA;
-    Trow.bind(S + (i < L.ME ? L.TT + i * L.TS : L.DUM), L.ME);
-    Tcol.bind(S + L.TT + (i < L.ME ? i : 0), L.TS);
+    Trow.bind(S + (i < L.KT ? L.TT + i * L.TS : L.DUM), L.KT);
+    Tcol.bind(S + L.TT + (i < L.KT ? i : 0), L.TS);
     GA.bind(S + L.GM + (ci < L.ME ? ci : 0) * L.GS, S + L.AC);
     Trow.zero_from(0);
     S[L.DUM + i] = 0.0;
