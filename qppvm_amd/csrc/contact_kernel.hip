@@ -86,18 +86,18 @@ struct ContactLayout {
             JD = TT + ov; ov += 6 * (1 + nc);
             const bool jc_in_xt = 6 * nc * NQ <= NR * QS;
             JC = jc_in_xt ? XT : TT + ov; ov += jc_in_xt ? 0 : 6 * nc * NQ;
-            PN = TT + ov; ov += 2 * NQ * 4;   // Gauss-Jordan pivot panel (rows < NQ publish)
-            RH = TT + ov; ov += 2 * 4 * NRC;  // its right-hand sides
+            PN = TT + ov; ov += 2 * NQ * kGjBS;   // Gauss-Jordan pivot panel (rows < NQ publish)
+            RH = TT + ov; ov += 2 * kGjBS * NRC;  // its right-hand sides
             HR = TT + ov; ov += NQ == 64 ? NQ * QS : 0; // H rows for a second rhs chunk
         } else {
             // The contact Jacobian rows are dead once H is assembled (a barrier precedes the
             // elimination), so the Gauss-Jordan panel reuses them: 22 KB -> 19.6 KB per instance
             // at n = 30, nc = 2, i.e. 8 instances per CU instead of 7
-            const int jcs = 6 * nc * NQ, gjs = 2 * NQ * 4 + 2 * 4 * NRC;
+            const int jcs = 6 * nc * NQ, gjs = 2 * NQ * kGjBS + 2 * kGjBS * NRC;
             ov = jcs > gjs ? jcs : gjs;
             JC = TT;                  // contact Jacobian rows (steps 1-3)
             PN = TT;                  // Gauss-Jordan pivot panel (rows < NQ publish; step 4)
-            RH = TT + 2 * NQ * 4;     // its right-hand sides
+            RH = TT + 2 * NQ * kGjBS;     // its right-hand sides
             HR = TT;                  // (unused: NQ == 64 && tr only)
         }
         // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns

@@ -50,7 +50,7 @@ namespace {
 // NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
 template <int NP>
 struct FastLayout {
-    static constexpr int BS = 4; // Gauss-Jordan pivot block
+    static constexpr int BS = kGjBS; // Gauss-Jordan pivot block
     int JR, PN, RH, U, WV, QD, F, RES, GR, PS, SIZE;
     __host__ __device__ FastLayout(int T, int m0)
     {

@@ -285,7 +285,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
 #pragma unroll
         for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
         __syncthreads();
-        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 8 * NP);
+        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
     }
     WBQ_STAMP(9);
     // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)

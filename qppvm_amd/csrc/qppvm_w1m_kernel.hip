@@ -57,8 +57,8 @@ struct W1mLayout {
             PS = TT + ov; ov += 24 * T;         // poses [R|p], ref
             F = TT + ov; ov += (6 * T + 1) & ~1; // task forces
             QD = TT + ov; ov += 64;
-            PN = TT + ov; ov += 2 * NQ * 4;     // Gauss-Jordan pivot panel
-            RH = TT + ov; ov += 2 * 4 * NRC;    // its right-hand sides
+            PN = TT + ov; ov += 2 * NQ * kGjBS;     // Gauss-Jordan pivot panel
+            RH = TT + ov; ov += 2 * kGjBS * NRC;    // its right-hand sides
             const int tt = KT * TS;
             o += tt > ov ? tt : ov;
         }

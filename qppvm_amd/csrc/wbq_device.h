@@ -207,6 +207,11 @@ __device__ double cart_error_component(const double *P, const double *Pr, int r)
 // right-hand sides per row; returns true if a pivot was not positive (M not SPD). On exit
 // rhs = M^-1 rhs (row i). PN: LDS [2][NP][4] panel, RH: LDS [2][4][RHS] pivot-row rhs.
 //
+#ifndef WBQ_GJ_BS
+#define WBQ_GJ_BS 4
+#endif
+constexpr int kGjBS = WBQ_GJ_BS; // Gauss-Jordan pivot block rows (panel: 2 x NP x kGjBS doubles)
+
 // Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing Schur
 // complement stays symmetric: pivot row k+r, column j, equals lane j's entry in column k+r.
 // Every lane publishes its BS panel entries; every lane factors the BS x BS pivot block D
@@ -217,7 +222,7 @@ __device__ double cart_error_component(const double *P, const double *Pr, int r)
 template <int NP, int NR, int RHS>
 __device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int n, int i, double *PN, double *RH)
 {
-    constexpr int BS = 4;
+    constexpr int BS = kGjBS;
     bool notspd = false;
     if (i < NP) {
 #pragma unroll

@@ -21,6 +21,9 @@ run bench 400 python bench.py --steps 200 --warmup 20 || exit 1
 if [ "$STEPS" = "all" ]; then
   run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu --no-pmc --no-variant || exit 1
   run bench_contact_cfg2 300 python bench.py --form contact --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
+  run bench_w1m 300 python bench.py --weight M --steps 100 --warmup 10 --no-cpu --no-variant || exit 1
+  run bench_w1m_cfg2 300 python bench.py --weight M --config 2 --steps 50 --warmup 5 --no-cpu --no-pmc --no-variant || exit 1
+  run bench_cfg4 300 python bench.py --config 4 --steps 5 --warmup 1 --no-cpu --no-pmc --no-variant || exit 1
   cd /tmp && run_dir="$GRAFT_REPO_ROOT/gpurun_out/prof"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$run_dir" -o run --output-format csv -- \
       python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu --no-pmc > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
