@@ -71,13 +71,22 @@ def test_contact_random(wbq_mod, oracle_lib, nc, masks):
     check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=96)
 
 
-@pytest.mark.parametrize("n,q", [(30, 0.85), (30, 0.7), (39, 0.8), (20, 0.8)])
-def test_contact_torque_rows(wbq_mod, oracle_lib, n, q):
-    """a12: actuated torque-limit rows, limits at a quantile of the free |tau| (rows bind)."""
-    free = ContactProblem(n=n, nc=4)
-    inp = contact_instances(free, 64, seed=70 + n, masks=MASKS4)
+@pytest.mark.parametrize("n,q,nc", [(30, 0.85, 4), (30, 0.7, 4), (39, 0.8, 4), (20, 0.8, 4), (14, 0.8, 4),
+                                    (30, 0.8, 2),
+                                    pytest.param(12, 0.8, 4, marks=pytest.mark.xfail(
+                                        strict=False,
+                                        reason="known gap: 1 of 64 instances (2 feet, 6 actuated joints) ends "
+                                               "in status 3 where the oracle solves; pre-dates the LDS overlays "
+                                               "(same with the b633dfd build; scripts/diag_contact_tr.py), "
+                                               "DESIGN.md section 8"))])
+def test_contact_torque_rows(wbq_mod, oracle_lib, n, q, nc):
+    """a12: actuated torque-limit rows, limits at a quantile of the free |tau| (rows bind).
+    n = 14, nc = 4 is the torque-row LDS layout whose contact Jacobian rows do not fit the
+    X^T region (they take the T-region overlay instead); n = 39 the 64-lane one."""
+    free = ContactProblem(n=n, nc=nc)
+    inp = contact_instances(free, 64, seed=70 + n, masks=MASKS4 if nc == 4 else None)
     tau_free = oracle_lib.contact_batch(free, inp)[0]
-    prob = ContactProblem(n=n, nc=4, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), q)))
+    prob = ContactProblem(n=n, nc=nc, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), q)))
     tau, x, st, _ = check_against_oracle(wbq_mod, oracle_lib, prob, inp)
     ok = st == 0
     assert ok.sum() >= 40
