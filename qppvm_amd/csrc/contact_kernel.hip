@@ -537,7 +537,11 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         __syncthreads();
     }
     {
-        ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, L.NX};
+        // rank cap of the loop: the rows never touch the forces of inactive contacts (their rows
+        // are disabled, their joint-row coefficients zero), so the rows span at most
+        // n + 3 * (active contacts) dimensions, not nx
+        const int dim = n + 3 * __popc((unsigned)cm & ((1u << nc) - 1u));
+        ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, dim};
         if constexpr (TR) {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
