@@ -57,15 +57,22 @@ def contact_bytes(n, nc):
     return inputs + outputs
 
 
-def build_workload(form, config, n, B, world, rank, device, weight=0):
+def shard_plan(config, B, world, global_batch):
+    """Weak scaling (configs 1, 2, 4): B instances per rank, rank r owns rows [r B, (r+1) B).
+    Config 3: a fixed global batch (65,536) in contiguous shards over the ranks (strong)."""
+    from qppvm_amd.shard import ShardPlan
+    return ShardPlan(global_batch if config == 3 else B * world, world)
+
+
+def build_workload(form, config, n, B, world, rank, device, weight=0, global_batch=65536):
     """(problem, inputs, solver class) for this rank's shard (weight: joint task W1 = I / M)."""
     from qppvm_amd.problem import ContactProblem, QPPVMProblem
-    from qppvm_amd.shard import ShardPlan
     from qppvm_amd.synth import contact_instances, qppvm_instances, replicate
     from qppvm_amd.wbq import ContactSolver, QPPVMSolver
-    plan = ShardPlan(B * world, world)  # weak scaling: rank r solves rows [r B, (r+1) B)
-    if config == 4:
-        config = 2  # MPC rollouts start from the config-2 random states
+    plan = shard_plan(config, B, world, global_batch)
+    B = plan.count(rank)
+    if config in (3, 4):
+        config = 2  # config 3 shards and MPC rollouts start from the config-2 random states
     if form == "qppvm":
         if config == 1:
             prob = QPPVMProblem(n=n, tau_max=1e6, joint_weight=weight)  # bounds inactive (SURVEY 8d config 1)
@@ -73,8 +80,10 @@ def build_workload(form, config, n, B, world, rank, device, weight=0):
         inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank))
         # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the first
         # B instances solved with the limits far away (same sample on every rank)
-        calib = inp if rank == 0 else qppvm_instances(QPPVMProblem(n=n), B, seed=1, offset=0)
-        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9, joint_weight=weight), max_batch=B, device=device)
+        # (the calibration sample is the first 4096 instances of the global batch, on every rank)
+        calib = qppvm_instances(QPPVMProblem(n=n), min(4096, plan.total), seed=1, offset=0)
+        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9, joint_weight=weight), max_batch=calib["h"].shape[0],
+                           device=device)
         tau_free, _, _ = free.solve_batch(calib)
         free.close()
         return (QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)), joint_weight=weight), inp,
@@ -85,8 +94,8 @@ def build_workload(form, config, n, B, world, rank, device, weight=0):
     free = ContactProblem(n=n, nc=4)
     masks = [0b0011, 0b0111, 0b1111]  # 2, 3 or 4 feet in contact
     inp = contact_instances(free, plan.count(rank), seed=1, offset=plan.start(rank), masks=masks)
-    calib = inp if rank == 0 else contact_instances(free, B, seed=1, offset=0, masks=masks)
-    s = ContactSolver(free, max_batch=B, device=device)
+    calib = contact_instances(free, min(4096, plan.total), seed=1, offset=0, masks=masks)
+    s = ContactSolver(free, max_batch=calib["h"].shape[0], device=device)
     tau_free, _, _ = s.solve_batch(calib)
     s.close()
     prob = ContactProblem(n=n, nc=4, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), 0.85)))
@@ -106,18 +115,22 @@ def churn_pool(form, prob, n, B, world, rank):
 
 
 def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False,
-        weight=0):
+        weight=0, global_batch=65536):
     """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
     import torch
-    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device, weight)
-    solver = Solver(prob, max_batch=B, device=device)
+    plan = shard_plan(config, B, world, global_batch)
+    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device, weight, global_batch)
+    B = plan.count(rank)
+    solver = Solver(prob, max_batch=max(B, 1), device=device)
     solver.set_inputs(inp)
     solver.sync()
     gather_buf = None
+    ag_events = []
     if allgather:
-        # tau goes straight into a torch tensor on torch's stream, then one RCCL all-gather
-        out = torch.empty((B, n), dtype=torch.float64, device="cuda")
-        gather_buf = torch.empty((world * B, n), dtype=torch.float64, device="cuda")
+        # tau goes straight into a torch tensor on torch's stream (padded to the largest shard),
+        # then one RCCL all-gather of every rank's shard over xGMI (SURVEY 8e)
+        out = torch.zeros((plan.max_count, n), dtype=torch.float64, device="cuda")
+        gather_buf = torch.empty((world * plan.max_count, n), dtype=torch.float64, device="cuda")
         solver.set_stream(torch.cuda.current_stream().cuda_stream)
         solver.set_device_outputs(out.data_ptr())
 
@@ -163,12 +176,21 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         else:
             solver.solve()
         if gather_buf is not None:
+            ev = None
+            if timing_on[0] and step_no[0] % TIMING_EVERY == 0:  # sampled, like the kernel events
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             if dist:
                 import torch.distributed as tdist
                 tdist.all_gather_into_tensor(gather_buf, out)
             else:
-                gather_buf.copy_(out)
+                gather_buf.copy_(out)  # world size 1: the gather is a device copy
+            if ev is not None:
+                ev[1].record()
+                ag_events.append(ev)
+        step_no[0] += 1
 
+    timing_on, step_no = [False], [0]
     for _ in range(warmup):
         step()
     solver.sync()
@@ -177,6 +199,7 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         import torch.distributed as tdist
         tdist.barrier()
     solver.set_timing(True, every=TIMING_EVERY)
+    timing_on[0], step_no[0] = True, 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -188,17 +211,22 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         tdist.barrier()
     dt = time.perf_counter() - t0
     solve_ms, kern_ms, launches = solver.get_timing_detail()
+    ag_ms = float(np.mean([a.elapsed_time(b) for a, b in ag_events])) if ag_events else 0.0
     tau, status, iters = solver.outputs()
+    if gather_buf is not None:  # the gathered tau holds this rank's shard where the plan puts it
+        g = gather_buf[rank * plan.max_count: rank * plan.max_count + B].cpu().numpy()
+        assert np.array_equal(g, tau), "all-gathered tau differs from the rank's own solve"
     solver.close()
     kavg_ms, savg_ms = kern_ms / max(launches, 1), solve_ms / max(launches, 1)
     if dist:
-        t = torch.tensor([dt, kavg_ms, savg_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt, kavg_ms, savg_ms, ag_ms], dtype=torch.float64, device="cuda")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt, kavg_ms, savg_ms = float(t[0]), float(t[1]), float(t[2])
+        dt, kavg_ms, savg_ms, ag_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
     per_inst = qppvm_bytes(n, prob.ntasks) if form == "qppvm" else contact_bytes(n, prob.nc)
     qps = HORIZON if config == 4 else 1  # an MPC step counts its N sequential QPs
     return dict(prob=prob, inp=inp, dt=dt, t_enq=t_enq, kavg_ms=kavg_ms, savg_ms=savg_ms, status=status, iters=iters,
-                bytes_per_instance=per_inst, total=B * world * steps * qps)
+                bytes_per_instance=per_inst, total=plan.total * steps * qps, B_local=B, allgather_ms=ag_ms,
+                allgather_bytes=8 * n * plan.max_count * world)
 
 
 def dominant_kernel(form, weight):
@@ -219,7 +247,8 @@ def pmc_traffic(args, form):
             cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "run", "--",
                    sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-pmc", "--no-variant",
                    "--steps", "20", "--warmup", "2", "--form", form, "--config", str(args.config),
-                   "--batch", str(args.batch), "--n", str(args.n), "--weight", args.weight]
+                   "--batch", str(args.batch), "--global-batch", str(args.global_batch), "--n", str(args.n),
+                   "--weight", args.weight]
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
@@ -262,11 +291,11 @@ def cpu_baseline(form, prob, inp, budget_s):
 
 def cpu_baseline_threads(form, prob, inp, budget_s):
     """Same oracle, one independent instance stream per host thread (the
-    all-cores run); the C calls release the GIL. Threads = the box's CPU share (16)."""
+    all-cores run); the C calls release the GIL. Threads = min(16, nproc): 16 is the GPU box's CPU share."""
     import concurrent.futures as cf
     import oracle
     fn = oracle.qppvm_batch if form == "qppvm" else oracle.contact_batch
-    T = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    T = max(1, min(16, len(os.sched_getaffinity(0))))  # the box's CPU share is 16 (nproc may show more)
     B = inp["h"].shape[0]
 
     def worker(w):
@@ -284,18 +313,53 @@ def cpu_baseline_threads(form, prob, inp, budget_s):
             "sample": f"{done} instances in {dt:.1f} s, {T} threads, one instance stream each"}
 
 
+def host_cpu():
+    """Host CPU description for the baseline: nproc (this process's affinity) and lscpu's model."""
+    info = {"nproc": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "CPU(s)", "Thread(s) per core", "Socket(s)"):
+                info["lscpu_" + k.strip().lower().replace(" ", "_").replace("(s)", "s")] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def relaunch(args):
+    """--gpus N > 1 from a plain process: one rank per GPU under torch.distributed.run, as a
+    child process started before this process touches the GPU (never an exec). Fails loudly
+    when the node has fewer GPUs."""
+    import socket
+
+    import torch
+    have = torch.cuda.device_count()  # counting devices does not initialise the GPU here
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) are visible", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU (configs 1, 2, 4)")
+    ap.add_argument("--global-batch", type=int, default=65536, help="config 3: instances over all GPUs")
     ap.add_argument("--n", type=int, default=30)
     ap.add_argument("--form", choices=("qppvm", "contact"), default="qppvm")
-    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 4),
+    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 3, 4),
                     help="1: identical instances; 2: random states, bounds / contacts churn; "
+                         "3: a fixed global batch of random states sharded over the GPUs + all-gather of tau; "
                          "4: MPC, each step = HORIZON sequential solves per rollout (wbq_rollout)")
-    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step")
+    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step (config 3: always)")
     ap.add_argument("--weight", choices=("I", "M"), default="I", help="QPPVM joint-task weight W1 (SURVEY 8a a6)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -305,15 +369,26 @@ def main():
                     help="PCIe-inclusive rate: host inputs copied in and outputs copied out every step "
                          "(never the headline value; DESIGN.md reports it beside it)")
     args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", "0"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    allgather = args.allgather or args.config == 3
     traffic, traffic_note = None, "skipped (--no-pmc or N > 1)"
     if not dist and not args.no_pmc:
         traffic, traffic_note = pmc_traffic(args, args.form)  # before this process touches the GPU
     import torch
+    if local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s)",
+              file=sys.stderr)
+        sys.exit(2)
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -322,20 +397,26 @@ def main():
     n, B = args.n, args.batch
     weight = 1 if args.weight == "M" else 0
     kern = dominant_kernel(args.form, weight)
-    m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, args.allgather, dist,
-            args.host_io, weight)
+    m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, allgather, dist,
+            args.host_io, weight, args.global_batch)
     value = m["total"] / m["dt"]
-    bpl = m["bytes_per_instance"] * B
+    bpl = m["bytes_per_instance"] * m["B_local"]
     achieved = bpl / (m["kavg_ms"] * 1e-3) / 1e9
     wl = {("qppvm", 1): "QPPVM 2-level torque QP, identical instances, bounds inactive (BASELINE config 1)",
           ("qppvm", 2): "QPPVM 2-level torque QP, random states, ~20% torque bounds active, 20% of the "
                         "instances re-randomised per call (D2D refresh in the step), warm start carried (config 2)",
+          ("qppvm", 3): f"QPPVM 2-level torque QP, {args.global_batch} random states (~20% torque bounds active) "
+                        "in contiguous shards over the GPUs, RCCL all-gather of tau every step (config 3)",
           ("contact", 1): "ForceAcc contact-form QP, double support (nc=2), identical instances (config 1 variant)",
           ("contact", 2): "ForceAcc contact-form QP, random states, 2-4 of 4 feet, torque rows, 20% of the "
                           "instances re-randomised per call (config 2)",
+          ("contact", 3): f"ForceAcc contact-form QP, {args.global_batch} random states (2-4 of 4 feet, torque rows) "
+                          "in contiguous shards over the GPUs, RCCL all-gather of tau every step (config 3)",
           ("qppvm", 4): f"MPC: rollouts x N={HORIZON} sequential QPPVM QPs, on-device semi-implicit Euler "
                         "(dt=1e-3), J/M/h frozen, warm-start carry (config 4)",
           ("contact", 4): f"MPC: rollouts x N={HORIZON} sequential contact-form QPs, on-device Euler (config 4)"}
+    per_gpu = f"batch={m['B_local']}/GPU" if args.config != 3 else f"global batch={args.global_batch}"
+    st, it = m["status"], m["iters"]
     line = {
         "metric": METRIC,
         "value": value,
@@ -345,14 +426,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": m["dt"] * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == 3 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic randomized robot states (SURVEY 8d), " + (
             "host inputs/outputs over PCIe every step (--host-io)" if args.host_io else "inputs resident in HBM"),
-        "config": {"workload": f"{wl[(args.form, args.config)]}{', W1 = M' if weight else ''}, n={n}, batch={B}/GPU",
-                   "global_batch": B * world, "n": n, "parallelism": f"shard{world}",
-                   "allgather": bool(args.allgather)},
+        "config": {"workload": f"{wl[(args.form, args.config)]}{', W1 = M' if weight else ''}, n={n}, {per_gpu}",
+                   "global_batch": m["total"] // (args.steps * (HORIZON if args.config == 4 else 1)), "n": n,
+                   "parallelism": f"shard{world}", "allgather": bool(allgather)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic["bytes"],
@@ -362,23 +443,30 @@ def main():
                      "traffic_note": traffic_note if traffic is None else
                      "rocprofv3 PMC per launch: 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE"
                      f"; raw fetch {traffic['fetch_raw']:.0f} B, write {traffic['write']:.0f} B"},
-        "status_ok_frac": float(np.mean(m["status"] == 0)),
-        "mean_active_set_steps": float(np.mean(m["iters"])),
+        "status_ok_frac": float(np.mean(st == 0)),
+        "status_histogram": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+        "mean_active_set_steps": float(np.mean(it)) if it.size else 0.0,
+        "max_active_set_steps": int(it.max()) if it.size else 0,
         "host_enqueue_us_per_step": m["t_enq"] * 1e6 / args.steps,
     }
-    if not args.no_variant and args.form == "qppvm":
+    if allgather:
+        line["allgather"] = {"avg_ms": m["allgather_ms"], "bytes": m["allgather_bytes"],
+                             "note": "torch.cuda events around all_gather_into_tensor (RCCL) on every "
+                                     f"{TIMING_EVERY}th step of the timed region, max over ranks; at N = 1 a device copy"}
+    if not args.no_variant and args.form == "qppvm" and args.config != 3:
         # the contact-form variant of the same config, same process, same protocol
         v = run("contact", args.config, n, B, max(50, args.steps // 2), args.warmup, world, rank, device,
                 False, dist)
-        va = v["bytes_per_instance"] * B / (v["kavg_ms"] * 1e-3) / 1e9
+        va = v["bytes_per_instance"] * v["B_local"] / (v["kavg_ms"] * 1e-3) / 1e9
         line["contact_variant"] = {"workload": wl[("contact", args.config)], "value": v["total"] / v["dt"],
                                    "ms_per_step": v["dt"] * 1e3 / max(50, args.steps // 2),
                                    "kernel_avg_us": v["kavg_ms"] * 1e3, "roofline_frac": va / HBM_PEAK_GBS,
                                    "status_ok_frac": float(np.mean(v["status"] == 0)),
                                    "mean_active_set_steps": float(np.mean(v["iters"]))}
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.form, m["prob"], m["inp"], args.cpu_seconds)
         line["cpu_baseline_threads"] = cpu_baseline_threads(args.form, m["prob"], m["inp"], args.cpu_seconds / 2)
+        line["cpu_host"] = host_cpu()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

@@ -143,7 +143,9 @@ typedef struct {
 
 int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out);
 int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out);
-/* Launch on a caller-provided hipStream_t (NULL = the context's own stream). */
+/* Launch on a caller-provided hipStream_t (NULL = the context's own stream). Solves of one
+ * context must stay stream-ordered: switch streams only between a completed solve and the next
+ * (a pending host-input copy made on the old stream is waited for). */
 int wbq_set_stream(wbq_ctx *ctx, void *hip_stream);
 int wbq_set_inputs(wbq_ctx *ctx, const wbq_inputs *in);
 int wbq_set_contact_inputs(wbq_ctx *ctx, const wbq_contact_inputs *in);
@@ -172,7 +174,9 @@ int wbq_set_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
 /* Device-resident outputs of the last solve (valid until the next wbq_solve/destroy). */
 int wbq_get_device_outputs(wbq_ctx *ctx, const double **tau, const int32_t **status,
                            const int32_t **iters);
-/* Drop the warm-start working set of instances with mask[b] != 0 (NULL = all). */
+/* Drop the warm-start working set of instances with mask[b] != 0, b < the current batch (the
+ * mask has one entry per instance of the last wbq_set_inputs batch); NULL = every instance up
+ * to max_batch. Stream-ordered with the solves. */
 int wbq_reset_warmstart(wbq_ctx *ctx, const uint8_t *mask);
 /* Kernel timing with HIP events on the launch stream: enable = N > 0 times every N-th solve
  * (events are stream packets: sampling keeps them from pacing the stream), 0 disables; then

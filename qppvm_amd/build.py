@@ -30,14 +30,24 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     lib = out or (LIB.replace("libwbq.so", "libwbq_diag.so") if diag else LIB)
     if not force and not diag and out is None and not _stale():
         return LIB
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-           "-I", os.path.join(ROOT, "include"),
-           *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", lib + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    flags = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
+             "-I", os.path.join(ROOT, "include"),
+             *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines]]
+    # one translation unit per process (each holds its own kernels), then one link
+    objs = [f"{lib}.{os.path.splitext(s)[0]}.o" for s in SOURCES]
+    procs = []
+    for s, o in zip(SOURCES, objs):
+        cmd = flags + ["-c", os.path.join(CSRC, s), "-o", o]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((cmd, subprocess.Popen(cmd)))
+    failed = [c for c, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", *objs, "-o", lib + ".tmp"])
+    for o in objs:
+        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 
@@ -46,23 +56,41 @@ PLUGIN_DIR = os.path.join(HERE, "plugins")
 PLUGIN_LIB = os.path.join(HERE, "libQPPVMPlugin.so")
 FORCEACC_LIB = os.path.join(HERE, "libForceAccPlugin.so")
 DRIVER = os.path.join(HERE, "qppvm_dummy_driver")
+# the same driver and shells against a row-major compat MatrixXd (tests/test_plugin.py: the
+# torques must not depend on the matrix storage order)
+DRIVER_RM = os.path.join(HERE, "qppvm_dummy_driver_rowmajor")
 
 
-def build_plugins(verbose: bool = False) -> tuple:
+def _plugin_sources():
+    out = []
+    for d in ("src", "include/QPPVM_RT_plugin", "include/ForceAccPlugin", "compat/XCM"):
+        base = os.path.join(PLUGIN_DIR, d)
+        out += [os.path.join(base, f) for f in os.listdir(base)]
+    return out
+
+
+def build_plugins(verbose: bool = False, force: bool = False) -> tuple:
     """The XBot plugin shells (libQPPVMPlugin.so and libForceAccPlugin.so, the reference's
-    target names, CMakeLists.txt:48-49) and the config-0 dummy-mode driver, host C++ over
-    libwbq.so."""
-    build()
+    target names, CMakeLists.txt:48-49) and the config-0 dummy-mode drivers, host C++ over
+    libwbq.so. Skipped when every output is newer than its sources and libwbq.so."""
+    lib = build()
+    outs = (PLUGIN_LIB, FORCEACC_LIB, DRIVER, DRIVER_RM)
+    deps = _plugin_sources() + [lib, os.path.join(ROOT, "include", "wbq.h")]
+    if not force and all(os.path.exists(o) for o in outs):
+        t = min(os.path.getmtime(o) for o in outs)
+        if all(os.path.getmtime(p) <= t for p in deps):
+            return PLUGIN_LIB, DRIVER, FORCEACC_LIB
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(PLUGIN_DIR, "compat"),
            "-I", os.path.join(PLUGIN_DIR, "include"), "-I", os.path.join(PLUGIN_DIR, "src")]
     link = ["-L", HERE, "-lwbq", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"]
     src = os.path.join(PLUGIN_DIR, "src", "QPPVMPlugin.cpp")
     fsrc = os.path.join(PLUGIN_DIR, "src", "ForceAcc.cpp")
+    drv = os.path.join(PLUGIN_DIR, "src", "dummy_driver.cpp")
     cmds = [
         ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", *inc, src, "-o", PLUGIN_LIB, *link],
         ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", *inc, fsrc, "-o", FORCEACC_LIB, *link],
-        ["g++", "-O2", "-std=c++17", "-Wall", *inc, os.path.join(PLUGIN_DIR, "src", "dummy_driver.cpp"), src, fsrc,
-         "-o", DRIVER, *link],
+        ["g++", "-O2", "-std=c++17", "-Wall", *inc, drv, src, fsrc, "-o", DRIVER, *link],
+        ["g++", "-O2", "-std=c++17", "-Wall", "-DXBOT_COMPAT_ROW_MAJOR", *inc, drv, src, fsrc, "-o", DRIVER_RM, *link],
     ]
     for c in cmds:
         if verbose:

@@ -249,25 +249,26 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
 
     // ------------------------------------------------------------------ 1. stage
     // unconditional buffer loads (clamped offsets, values selected afterwards): one HBM trip
-    const long Bn = (long)a.B * n;
-    const int voff = (int)(8 * (b * n + ic));
-    const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
-    const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    // buffer resources start at this block's instance: per-lane offsets stay small
+    const long B = a.B;
+    const int voff = (int)(8 * ic);
+    const double q_i = bload(rsrc_at(a.q, b, B, n), voff, 0), qd_i = bload(rsrc_at(a.qd, b, B, n), voff, 0);
+    const double qref_i = bload(rsrc_at(a.qref, b, B, n), voff, 0), h_i0 = bload(rsrc_at(a.h, b, B, n), voff, 0);
     double mrow[NQ]; // M is symmetric: lane i's row is its column, so the loads coalesce
     {
-        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-        const int moff = (int)(8 * (b * n * n + ic));
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
+        const int moff = (int)(8 * ic);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     }
     double jc[6 * kCMax], jw[6];
     {
-        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.Jc, Bn * nc * 6);
-        const int joff = (int)(8 * (b * nc * 6 * n + ic));
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
+        const int joff = (int)(8 * ic);
 #pragma unroll
         for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = bload(Jrs, joff, 8 * (rr < 6 * nc ? rr : 6 * nc - 1) * n);
-        const __amdgpu_buffer_rsrc_t Wrs = rsrc(a.Jw, Bn * 6);
-        const int woff = (int)(8 * (b * 6 * n + ic));
+        const __amdgpu_buffer_rsrc_t Wrs = rsrc_at(a.Jw, b, B, 6L * n);
+        const int woff = (int)(8 * ic);
 #pragma unroll
         for (int r = 0; r < 6; ++r) jw[r] = bload(Wrs, woff, 8 * r * n);
     }
@@ -560,13 +561,13 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     if (ok && qrow) { // joint row i: M_i qdd - J_c,i^T f + h_i
         double t = h_i;
         // lane i's own M row and contact-Jacobian column, re-read (L2) rather than held
-        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-        const int moff = (int)(8 * (b * n * n + ic));
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
+        const int moff = (int)(8 * ic);
         double mr[NQ], jr[3 * kCMax]; // unconditional (clamped) loads: one round trip
 #pragma unroll
         for (int j = 0; j < NQ; ++j) mr[j] = bload(Mrs, moff, 8 * (j < n ? j : n - 1) * n);
-        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.Jc, Bn * nc * 6);
-        const int joff = (int)(8 * (b * nc * 6 * n + ic));
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
+        const int joff = (int)(8 * ic);
 #pragma unroll
         for (int f = 0; f < 3 * kCMax; ++f)
             jr[f] = bload(Jrs, joff, 8 * (6 * (f < nf ? f / 3 : 0) + f % 3) * n);
@@ -597,17 +598,12 @@ template <int NQ, bool TR, int KMR>
 hipError_t launch_t(const ContactArgs &a, hipStream_t stream)
 {
     constexpr int NRC = TR ? 40 : 16;
-    static size_t attr = 0;
     const ContactLayout L(a.n, a.nc, TR, NQ, NRC);
     if (L.NR > NRC * ((NQ == 64 && TR) ? 2 : 1) || L.ME > 64 || L.NX > 64) return hipErrorInvalidValue;
     if (!TR && L.ME > KMR) return hipErrorInvalidValue; // the register slot vectors hold every active row
     const size_t lds = sizeof(double) * L.SIZE;
-    if (lds > attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)contact_kernel<NQ, TR, KMR>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = lds;
-    }
+    const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR>, lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }

@@ -131,14 +131,14 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     const int n = a.n, m0 = a.m0;
     const ActiveLayout<NP> L(a.ntasks, m0);
     const int ic = i < n ? i : n - 1;
-    const int moff = (int)(8 * (b * n * n + ic));
-    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, (long)a.B * n * n);
-    // M rows (columns, coalesced)
+    // M rows (columns, coalesced); 64-bit addressing: the instances of a wave come from a work
+    // list here, so no wave-uniform base exists for a buffer resource
+    const double *Mb = a.M + b * n * n + ic;
     RowStore<NP, MREG> Mr;
     Mr.bind(S + L.MA + i * RS);
     double mrow[NP];
 #pragma unroll
-    for (int r = 0; r < NP; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    for (int r = 0; r < NP; ++r) mrow[r] = Mb[(r < n ? r : n - 1) * n];
 #pragma unroll
     for (int r = 0; r < NP; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
     if constexpr (MREG) {
@@ -384,6 +384,12 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(cons
         const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status,
                                             iters, infeasible);
         WBQ_STAMP(12);
+#ifdef WBQ_STAMPS
+        if (threadIdx.x == 0 && a.stamps) { // step counts of the diagnostic build
+            a.stamps[blockIdx.x * kStamps + 13] = (unsigned long long)ro.it;
+            a.stamps[blockIdx.x * kStamps + 14] = (unsigned long long)iters;
+        }
+#endif
         if (infeasible && status == 0) status = 2;
         double tau_i = x_i + h_i;
         if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
@@ -424,10 +430,11 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     // ---------------------------------------------------------------- 1. stage
     // Every global load is unconditional (clamped offsets, values selected afterwards), so
     // they issue back to back: one HBM round trip.
-    const long Bn = (long)a.B * n;
-    const int voff = (int)(8 * (bn + ic));
-    const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
-    const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    // buffer resources start at the wave's first instance b0: per-lane offsets stay small
+    const long b0 = (long)blockIdx.x * IPW, lb = valid ? b - b0 : 0, B = a.B;
+    const int voff = (int)(8 * (lb * n + ic));
+    const double q_i = bload(rsrc_at(a.q, b0, B, n), voff, 0), qd_i = bload(rsrc_at(a.qd, b0, B, n), voff, 0);
+    const double qref_i = bload(rsrc_at(a.qref, b0, B, n), voff, 0), h_i0 = bload(rsrc_at(a.h, b0, B, n), voff, 0);
     // the warm-start hint is issued before the bulk loads: vmcnt retires in order, so a load
     // issued after M and waited for early would drain all of M with it
     const unsigned char hint_b = a.ws_hint[valid ? b : 0]; // unconditional: no branch on it here
@@ -435,17 +442,17 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     // qd) can start while M is still streaming in
     double jv[kTMax * 6];
     {
-        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.J, Bn * T * 6);
-        const int joff = (int)(8 * ((valid ? b * T * 6 * n : 0) + ic));
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.J, b0, B, (long)T * 6 * n);
+        const int joff = (int)(8 * (lb * T * 6 * n + ic));
 #pragma unroll
         for (int rr = 0; rr < kTMax * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
     }
     constexpr int kPoseIt = (kTMax * 24 + NP - 1) / NP;
     double pv[kPoseIt];
     {
-        const long base = valid ? b * T * 12 : 0;
-        const __amdgpu_buffer_rsrc_t Prs = rsrc(a.pose, (long)a.B * T * 12);
-        const __amdgpu_buffer_rsrc_t Rrs = rsrc(a.pose_ref, (long)a.B * T * 12);
+        const long base = lb * T * 12;
+        const __amdgpu_buffer_rsrc_t Prs = rsrc_at(a.pose, b0, B, (long)T * 12);
+        const __amdgpu_buffer_rsrc_t Rrs = rsrc_at(a.pose_ref, b0, B, (long)T * 12);
 #pragma unroll
         for (int it = 0; it < kPoseIt; ++it) {
             int e = it * NP + i;
@@ -457,8 +464,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             pv[it] = (c < 12) ? p0 : p1;
         }
     }
-    const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-    const int moff = (int)(8 * ((valid ? b * n * n : 0) + ic));
+    const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b0, B, (long)n * n);
+    const int moff = (int)(8 * (lb * n * n + ic));
     // M is symmetric: lane i's row is its column, so row r of M read across lanes is
     // contiguous -- coalesced loads straight into the elimination registers.
     double A[NP];
@@ -715,15 +722,12 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
 }
 
 template <int NP, typename Lay, typename K>
-hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t stream, size_t &attr_set)
+hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t stream)
 {
     constexpr int IPW = kWave / NP;
     const size_t lds = sizeof(double) * Lay(a.ntasks, a.m0).SIZE * IPW;
-    if (lds > attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = lds;
-    }
+    const hipError_t e = ensure_dynamic_lds((const void *)kern, lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, a);
     return hipGetLastError();
 }
@@ -732,12 +736,10 @@ template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     constexpr int IPW = kWave / NP;
-    static size_t attr_fast = 0, attr_active = 0, attr_repair = 0;
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
     constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
-    hipError_t e = launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED>, a, grid, stream,
-                                                             attr_fast);
+    hipError_t e = launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED>, a, grid, stream);
     if (e != hipSuccess) return e;
     if (mid) { // end of the dominant launch
         e = hipEventRecord(mid, stream);
@@ -745,14 +747,12 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     // follow-up kernels: grid-stride over their work lists, at most kFollowGrid blocks
     const unsigned fgrid = grid < kFollowGrid ? grid : kFollowGrid;
-    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream, attr_active);
+    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream);
     if (e != hipSuccess) return e;
-    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream, attr_repair);
+    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
 }
 
 }  // namespace
-
-bool qppvm_single_launch(int) { return false; }
 
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {

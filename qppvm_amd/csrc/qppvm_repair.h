@@ -277,11 +277,11 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
     // are rebuilt below)
     {
-        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, (long)a.B * n * n);
-        const int moff = (int)(8 * (b * n * n + ic));
+        // 64-bit addressing: the instances of a wave come from a work list (no uniform base)
+        const double *Mb = a.M + b * n * n + ic;
         double A[NP];
 #pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+        for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
 #pragma unroll
         for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
         __syncthreads();

@@ -143,37 +143,38 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
 
     // ------------------------------------------------------------------ 1. stage
     // unconditional buffer loads (clamped offsets, values selected afterwards): one HBM trip
-    const long Bn = (long)a.B * n;
-    const int voff = (int)(8 * (b * n + ic));
-    const double q_i = bload(rsrc(a.q, Bn), voff, 0), qd_i = bload(rsrc(a.qd, Bn), voff, 0);
-    const double qref_i = bload(rsrc(a.qref, Bn), voff, 0), h_i0 = bload(rsrc(a.h, Bn), voff, 0);
+    // buffer resources start at the instance (one per wave): per-lane offsets stay small
+    const long bu = uniform_long(b), B = a.B;
+    const int voff = (int)(8 * ic);
+    const double q_i = bload(rsrc_at(a.q, bu, B, n), voff, 0), qd_i = bload(rsrc_at(a.qd, bu, B, n), voff, 0);
+    const double qref_i = bload(rsrc_at(a.qref, bu, B, n), voff, 0), h_i0 = bload(rsrc_at(a.h, bu, B, n), voff, 0);
     double jv[kTMax * 6];
     {
-        const __amdgpu_buffer_rsrc_t Jrs = rsrc(a.J, Bn * T * 6);
-        const int joff = (int)(8 * (b * T * 6 * n + ic));
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.J, bu, B, (long)T * 6 * n);
+        const int joff = (int)(8 * ic);
 #pragma unroll
         for (int rr = 0; rr < kTMax * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
     }
     constexpr int kPoseIt = (kTMax * 24 + 63) / 64;
     double pv[kPoseIt];
     {
-        const __amdgpu_buffer_rsrc_t Prs = rsrc(a.pose, (long)a.B * T * 12);
-        const __amdgpu_buffer_rsrc_t Rrs = rsrc(a.pose_ref, (long)a.B * T * 12);
+        const __amdgpu_buffer_rsrc_t Prs = rsrc_at(a.pose, bu, B, (long)T * 12);
+        const __amdgpu_buffer_rsrc_t Rrs = rsrc_at(a.pose_ref, bu, B, (long)T * 12);
 #pragma unroll
         for (int it = 0; it < kPoseIt; ++it) {
             int e = it * 64 + i;
             e = e < T * 24 ? e : T * 24 - 1;
             const int t = e / 24, c = e - t * 24;
             const int cc = c < 12 ? c : c - 12;
-            const double p0 = bload(Prs, (int)(8 * (b * T * 12 + t * 12 + cc)), 0);
-            const double p1 = bload(Rrs, (int)(8 * (b * T * 12 + t * 12 + cc)), 0);
+            const double p0 = bload(Prs, (int)(8 * (t * 12 + cc)), 0);
+            const double p1 = bload(Rrs, (int)(8 * (t * 12 + cc)), 0);
             pv[it] = (c < 12) ? p0 : p1;
         }
     }
     double A[NQ]; // M is symmetric: lane i's row is its column, so the loads coalesce
     {
-        const __amdgpu_buffer_rsrc_t Mrs = rsrc(a.M, Bn * n);
-        const int moff = (int)(8 * (b * n * n + ic));
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, bu, B, (long)n * n);
+        const int moff = (int)(8 * ic);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     }
@@ -461,18 +462,13 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
 template <int NQ, int M0>
 hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
-    static size_t attr_main = 0, attr_rep = 0;
     const W1mLayout L(a.n, a.ntasks, a.m0, NQ, 1 + M0);
     if (L.ME > 64) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
-    if (lds > attr_main) {
-        hipError_t e = hipFuncSetAttribute((const void *)qppvm_w1m_kernel<NQ, M0>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_main = lds;
-    }
+    hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0>, lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((qppvm_w1m_kernel<NQ, M0>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (mid) {
         e = hipEventRecord(mid, stream);
@@ -480,12 +476,8 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     const int ws = ActiveLayout<64>(a.ntasks, a.m0).SIZE;
     const size_t lds2 = sizeof(double) * ((ws > L.SIZE ? ws : L.SIZE) + RepairIn::SIZE);
-    if (lds2 > attr_rep) {
-        e = hipFuncSetAttribute((const void *)qppvm_w1m_repair_kernel<NQ, M0>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
-        if (e != hipSuccess) return e;
-        attr_rep = lds2;
-    }
+    e = ensure_dynamic_lds((const void *)qppvm_w1m_repair_kernel<NQ, M0>, lds2);
+    if (e != hipSuccess) return e;
     const unsigned grid = a.B < (int)kFollowGrid ? (unsigned)a.B : kFollowGrid;
     hipLaunchKernelGGL((qppvm_w1m_repair_kernel<NQ, M0>), dim3(grid), dim3(64), lds2, stream, a);
     return hipGetLastError();

@@ -8,7 +8,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/wbq.h"
@@ -32,6 +35,7 @@ struct wbq_ctx {
     // back for the current batch, so a host-side set_inputs is a single H2D copy
     double *dev_in = nullptr, *host_in = nullptr;
     hipEvent_t in_copied = nullptr;
+    hipStream_t in_stream = nullptr; // stream the last host-input copy was issued on
     bool in_pending = false;
     const double *in[16] = {};
     const int *cmask = nullptr; // contact form: [B] (packed after the fp64 fields when staged)
@@ -69,6 +73,25 @@ struct wbq_ctx {
     size_t np = 0;
     int epoch = 0;
 };
+
+namespace wbq {
+
+hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> done; // (device, kernel) -> limit set
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    size_t &cur = done[{dev, kernel}];
+    if (bytes <= cur) return hipSuccess;
+    e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) cur = bytes;
+    return e;
+}
+
+}  // namespace wbq
 
 namespace {
 
@@ -368,6 +391,7 @@ int wbq_set_contact_inputs(wbq_ctx *c, const wbq_contact_inputs *in)
             WBQ_HIP(hipMemcpyAsync(c->dev_in, c->host_in, off * 8, hipMemcpyHostToDevice, c->stream));
             WBQ_HIP(hipEventRecord(c->in_copied, c->stream));
             c->in_pending = true;
+            c->in_stream = c->stream;
         }
     }
     c->batch = in->batch;
@@ -424,6 +448,7 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
             WBQ_HIP(hipMemcpyAsync(c->dev_in, c->host_in, off * 8, hipMemcpyHostToDevice, c->stream));
             WBQ_HIP(hipEventRecord(c->in_copied, c->stream));
             c->in_pending = true;
+            c->in_stream = c->stream;
         }
     }
     c->batch = in->batch;
@@ -439,6 +464,14 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt)
 {
     if (!c) return WBQ_E_INVALID;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "wbq_set_inputs not called");
+    if (c->in_pending && c->in_stream != c->stream) {
+        // the stream was switched after the host inputs were copied: order the solve behind
+        // that copy (the epoch-parity work counters also need the solves stream-ordered, so a
+        // context should otherwise stay on one stream between solves)
+        WBQ_HIP(hipSetDevice(c->device));
+        WBQ_HIP(hipStreamWaitEvent(c->stream, c->in_copied, 0));
+        c->in_stream = c->stream;
+    }
     if (c->form == WBQ_FORM_CONTACT) return solve_contact(c, integrate, dt);
     wbq::QppvmArgs a{};
     a.B = c->batch;
@@ -485,14 +518,12 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt)
     // timed solves record (start, after the dominant first kernel, end) on the launch stream
     const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
                        (c->solves++ % (unsigned long long)c->timing_every) == 0;
-    const bool single = wbq::qppvm_single_launch(a.n);
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
-    WBQ_HIP(wbq::launch_qppvm(a, c->stream, (timed && !single) ? c->ev[c->ev_used + 1] : nullptr));
+    WBQ_HIP(wbq::launch_qppvm(a, c->stream, timed ? c->ev[c->ev_used + 1] : nullptr));
     if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
     if (timed) {
-        // one launch: the end event also ends the dominant kernel (no extra event in the stream)
         WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 2], c->stream));
-        c->ev_mid[c->ev_used / 3] = single ? 2 : 1;
+        c->ev_mid[c->ev_used / 3] = 1;
         c->ev_used += 3;
     }
     return WBQ_SUCCESS;
@@ -598,7 +629,7 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
     if (!c) return WBQ_E_INVALID;
     if (!c->ws_hint) return WBQ_SUCCESS; // no warm-start state in this form
     WBQ_HIP(hipSetDevice(c->device));
-    const int B = c->d.max_batch;
+    const int B = mask ? c->batch : c->d.max_batch; // a mask has one entry per instance of the batch
     int b = 0;
     while (b < B) {
         if (mask && !mask[b]) {

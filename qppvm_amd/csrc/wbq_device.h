@@ -57,6 +57,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double *p, long ele
     return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
                                              0x00020000);
 }
+// A value every lane holds alike, moved to SGPRs (v_readfirstlane) so that what is built
+// from it (a buffer resource) is wave-uniform.
+__device__ __forceinline__ long uniform_long(long v)
+{
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Resource over instances [b0, B) of a field with `per` elements per instance. b0 is the
+// first instance of the wave (wave-uniform, so the descriptor stays in SGPRs): the 32-bit
+// per-lane byte offsets then only span the instances of one wave, never the whole batch, so
+// no batch size reaches the 2^31-byte offset limit.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const double *p, long b0, long B, long per)
+{
+    return rsrc(p + b0 * per, (B - b0) * per);
+}
 __device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes)
 {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff_bytes, soff_bytes, 0));

@@ -55,10 +55,12 @@ struct QppvmArgs {
 
 constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
 
+// Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
+// device and kernel; thread-safe: contexts on several devices or threads share it).
+hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes);
+
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
-// mid (optional): recorded on the stream right after the first (dominant) kernel when a
-// second launch follows (n > 32); n <= 32 is one launch (qppvm_single_launch).
-bool qppvm_single_launch(int n);
+// mid (optional): recorded on the stream right after the first (dominant) kernel.
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 // W1 = M (joint_weight 1): main kernel + level-0 repair kernel; needs m0 + n <= 64
 hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);

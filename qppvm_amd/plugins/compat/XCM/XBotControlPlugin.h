@@ -11,7 +11,7 @@
 //                         computeJdotQdot, getPointPosition
 //   REGISTER_XBOT_PLUGIN(name, class) -> extern "C" factory symbols
 // Building against the real XCM is an install-time swap of this include directory; the
-// linear-algebra types below stand in for Eigen's (row-major, fp64).
+// linear-algebra types below stand in for Eigen's (column-major MatrixXd, fp64).
 #pragma once
 
 #include <cstddef>
@@ -41,7 +41,9 @@ private:
     std::vector<double> d_;
 };
 
-// row-major dense matrix
+// dense matrix; column-major storage like Eigen's default MatrixXd (XBOT_COMPAT_ROW_MAJOR
+// switches to row-major: the plugin shells read elements by (row, col), never through data(),
+// so their results do not depend on the storage order -- tests/test_plugin.py checks both)
 class MatrixXd {
 public:
     MatrixXd() = default;
@@ -49,8 +51,13 @@ public:
     std::size_t rows() const { return r_; }
     std::size_t cols() const { return c_; }
     void resize(std::size_t r, std::size_t c) { r_ = r; c_ = c; d_.assign(r * c, 0.0); }
+#ifdef XBOT_COMPAT_ROW_MAJOR
     double &operator()(std::size_t i, std::size_t j) { return d_[i * c_ + j]; }
     double operator()(std::size_t i, std::size_t j) const { return d_[i * c_ + j]; }
+#else
+    double &operator()(std::size_t i, std::size_t j) { return d_[j * r_ + i]; }
+    double operator()(std::size_t i, std::size_t j) const { return d_[j * r_ + i]; }
+#endif
     double *data() { return d_.data(); }
     const double *data() const { return d_.data(); }
 
@@ -87,6 +94,11 @@ public:
     virtual bool getMotorPosition(Eigen::VectorXd &q) const = 0;
     virtual bool getMotorVelocity(Eigen::VectorXd &qd) const = 0;
     virtual bool setReferenceFrom(const ModelInterface &model, Sync::Flag flag) = 0;
+    // XBotInterface takes several Sync flags at once (ForceAcc.cpp:242: Position, Effort)
+    bool setReferenceFrom(const ModelInterface &model, Sync::Flag a, Sync::Flag b)
+    {
+        return setReferenceFrom(model, static_cast<Sync::Flag>(a | b));
+    }
     virtual bool move() = 0;
 };
 

@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include "abi_copy.h"
+
 REGISTER_XBOT_PLUGIN(ForceAccExample, XBotPlugin::ForceAccExample)
 
 using namespace XBotPlugin;
@@ -87,7 +89,7 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     Eigen::VectorXd v;
     Eigen::Affine3d P;
     _model->getInertiaMatrix(M);
-    std::memcpy(_in[0].data(), M.data(), sizeof(double) * n * n);
+    copy_row_major(M, n, n, _in[0].data()); // element-wise: Eigen's MatrixXd is column-major
     _model->computeNonlinearTerm(_h);
     std::memcpy(_in[1].data(), _h.data(), sizeof(double) * n);
     _model->getJointPosition(_q);
@@ -96,7 +98,7 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     std::memcpy(_in[3].data(), _qdot.data(), sizeof(double) * n);
     std::memcpy(_in[4].data(), _q_ref.data(), sizeof(double) * n);
     _model->getJacobian(_waist_link, J);
-    std::memcpy(_in[5].data(), J.data(), sizeof(double) * 6 * n);
+    copy_row_major(J, 6, n, _in[5].data());
     _model->computeJdotQdot(_waist_link, v);
     std::memcpy(_in[6].data(), v.data(), sizeof(double) * 6);
     _model->getPose(_waist_link, P);
@@ -104,7 +106,7 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     std::memcpy(_in[8].data(), _waist_ref.m, sizeof(P.m));
     for (size_t c = 0; c < nc; ++c) {
         _model->getJacobian(_contact_links[c], J);
-        std::memcpy(_in[9].data() + c * 6 * n, J.data(), sizeof(double) * 6 * n);
+        copy_row_major(J, 6, n, _in[9].data() + c * 6 * n);
         _model->computeJdotQdot(_contact_links[c], v);
         std::memcpy(_in[10].data() + c * 6, v.data(), sizeof(double) * 6);
         _model->getPose(_contact_links[c], P);
@@ -146,7 +148,7 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     _model->setJointEffort(_tau);                        // :219
     _robot->setStiffness(_k);                            // :239-241 (re-sent every tick)
     _robot->setDamping(_d);
-    _robot->setReferenceFrom(*_model, XBot::Sync::Effort);
+    _robot->setReferenceFrom(*_model, XBot::Sync::Position, XBot::Sync::Effort); // :242
     _robot->move(); // :248
 }
 

@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include "abi_copy.h"
+
 REGISTER_XBOT_PLUGIN(QPPVMPlugin, demo::QPPVMPlugin)
 
 using namespace demo;
@@ -95,11 +97,13 @@ void QPPVMPlugin::QPPVMControl(double /*time*/) // :201-259
 {
     const int n = _model->getJointNum();
     Eigen::MatrixXd M, J;
+    // element-wise into the ABI's row-major layout (include/wbq.h): Eigen's MatrixXd is
+    // column-major, so its data() is never copied as is
     _model->getInertiaMatrix(M);
-    std::memcpy(_M.data(), M.data(), sizeof(double) * n * n);
+    copy_row_major(M, n, n, _M.data());
     for (int t = 0; t < 2; ++t) {
         _model->getJacobian(_ee_links[t], J);
-        std::memcpy(_J.data() + (size_t)t * 6 * n, J.data(), sizeof(double) * 6 * n);
+        copy_row_major(J, 6, n, _J.data() + (size_t)t * 6 * n);
         Eigen::Affine3d P;
         _model->getPose(_ee_links[t], P);
         std::memcpy(_pose.data() + 12 * t, P.m, sizeof(P.m));

@@ -10,10 +10,12 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include <ForceAccPlugin/ForceAcc.h>
 #include <QPPVM_RT_plugin/QPPVMPlugin.h>
 
+#include "abi_copy.h"
 #include "dummy_robot.h"
 
 // ForceAcc in dummy mode: dump = header (n, nc, ticks), then per tick the 13 staged solver
@@ -63,8 +65,8 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
     if (f) std::fclose(f);
     plugin.close();
     std::printf("{\"config\": 0, \"plugin\": \"ForceAccExample\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
-                "\"run_us\": %.3f, \"worst_us\": %.3f, \"solver_errors\": %d}\n", n, ticks, total / ticks,
-                run_total / ticks, worst, plugin.solver_errors());
+                "\"run_us\": %.3f, \"worst_us\": %.3f, \"solver_errors\": %d, \"sync_flags\": %d}\n", n, ticks,
+                total / ticks, run_total / ticks, worst, plugin.solver_errors(), handle->robot().last_sync());
     return 0;
 }
 
@@ -132,10 +134,13 @@ int main(int argc, char **argv)
             m.getJointPosition(q);
             m.getJointVelocity(qd);
             m.computeNonlinearTerm(h);
-            std::fwrite(M.data(), sizeof(double), (size_t)n * n, f);
+            std::vector<double> rm((size_t)6 * n > (size_t)n * n ? (size_t)6 * n : (size_t)n * n);
+            copy_row_major(M, n, n, rm.data());
+            std::fwrite(rm.data(), sizeof(double), (size_t)n * n, f);
             for (const char *link : {"arm2_7", "arm1_7"}) {
                 m.getJacobian(link, J);
-                std::fwrite(J.data(), sizeof(double), (size_t)6 * n, f);
+                copy_row_major(J, 6, n, rm.data());
+                std::fwrite(rm.data(), sizeof(double), (size_t)6 * n, f);
             }
             for (const char *link : {"arm2_7", "arm1_7"}) {
                 Eigen::Affine3d P;

@@ -184,11 +184,15 @@ public:
     bool setDamping(const Eigen::VectorXd &d) override { d_ = d; return true; }
     bool getMotorPosition(Eigen::VectorXd &q) const override { q = q_; return true; }
     bool getMotorVelocity(Eigen::VectorXd &qd) const override { qd = qd_; return true; }
-    bool setReferenceFrom(const XBot::ModelInterface &model, XBot::Sync::Flag) override
+    using XBot::RobotInterface::setReferenceFrom;
+    bool setReferenceFrom(const XBot::ModelInterface &model, XBot::Sync::Flag flag) override
     {
-        model.getJointEffort(tau_);
+        if (flag & XBot::Sync::Effort) model.getJointEffort(tau_);
+        if (flag & XBot::Sync::Position) model.getJointPosition(qref_);
+        last_sync_ = flag;
         return true;
     }
+    int last_sync() const { return last_sync_; }
     bool move() override { return true; }
     void set_state(const Eigen::VectorXd &q, const Eigen::VectorXd &qd) { q_ = q; qd_ = qd; }
     // dummy-mode kinematic step with a given acceleration (the integration the reference
@@ -208,7 +212,9 @@ public:
         Eigen::VectorXd h;
         model.getInertiaMatrix(M);
         model.computeNonlinearTerm(h);
-        std::vector<double> L(M.data(), M.data() + (size_t)n_ * n_), a(n_);
+        std::vector<double> L((size_t)n_ * n_), a(n_);
+        for (int r = 0; r < n_; ++r)
+            for (int c = 0; c < n_; ++c) L[(size_t)r * n_ + c] = M(r, c);
         for (int j = 0; j < n_; ++j) a[j] = tau_[j] - h[j];
         cholesky_solve(L, a);
         for (int j = 0; j < n_; ++j) {
@@ -244,8 +250,9 @@ private:
         }
     }
     int n_;
-    Eigen::VectorXd q_, qd_, k_, d_;
+    Eigen::VectorXd q_, qd_, k_, d_, qref_;
     mutable Eigen::VectorXd tau_;
+    int last_sync_ = 0;
 };
 
 class Handle : public XBot::Handle {

@@ -72,6 +72,14 @@ def load_library(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise WbqError(f"{path} not built: run `python -m qppvm_amd.build` (hipcc, gfx950)")
+    try:
+        # One HIP runtime per process: torch ships its own libamdhip64 / libhsa-runtime64 with the
+        # same sonames as /opt/rocm's. Loaded first, torch's copies also serve libwbq, so torch
+        # tensors, streams and libwbq contexts share one runtime; loaded second, torch finds
+        # /opt/rocm's runtime already in the process and sees no GPU.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P, I = ctypes.c_void_p, ctypes.c_int
     lib.wbq_create.argtypes = [ctypes.POINTER(Desc), I, ctypes.POINTER(P)]
@@ -229,7 +237,11 @@ class QPPVMSolver:
         return self.outputs()
 
     def reset_warmstart(self, mask=None):
+        """Drop the warm start of the instances with mask[b] != 0 (one entry per instance of the
+        current batch; None = all)."""
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        if m is not None and m.shape != (self.batch,):
+            raise ValueError(f"mask must have one entry per instance of the batch ({self.batch}), got {m.shape}")
         self._check(self.lib.wbq_reset_warmstart(self.ctx, None if m is None else _ptr(m)),
                     "wbq_reset_warmstart")
 

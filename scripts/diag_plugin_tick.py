@@ -1,0 +1,65 @@
+"""Diagnostics (GPU box): where a config-0 QPPVMPlugin tick goes. Runs the dummy driver with a dump
+of its first ticks' solver inputs, then re-solves those ticks one instance per solve (warm start
+carried, as in the plugin) with the phase-stamp build (libwbq_diag.so): per tick the device time
+of the solve, the repair phases (Gauss-Jordan, BVLS, pins + equality, dual active set) in shader
+cycles, and the BVLS / active-set step counts."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    from test_plugin import read_dump
+
+    from qppvm_amd import wbq
+    from qppvm_amd.problem import QPPVMProblem
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "diag_plugin_tick.json")
+    lib = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "qppvm_amd", "libwbq_diag.so")
+    ticks = int(os.environ.get("DIAG_TICKS", "40"))
+    dump = "/tmp/diag_tick_dump.bin"
+    subprocess.run([os.path.join(ROOT, "qppvm_amd", "qppvm_dummy_driver"), "--ticks", str(ticks), "--dump", dump,
+                    str(ticks)], check=True, capture_output=True)
+    n, d = read_dump(dump)
+    prob = QPPVMProblem(n=n, tau_max=150.0)
+    wbq._lib = None
+    wbq.load_library(lib)
+    s = wbq.QPPVMSolver(prob, max_batch=1)
+    s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    K = 16
+    rows = []
+    for t in range(ticks):
+        inp = {k: np.ascontiguousarray(d[k][t:t + 1]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
+        inp["pose"] = inp["pose"].reshape(1, 2, 12)
+        inp["pose_ref"] = inp["pose_ref"].reshape(1, 2, 12)
+        s.set_inputs(inp)
+        s.sync()
+        s.set_timing(True)
+        s.solve()
+        s.sync()
+        ms, _ = s.get_timing()
+        buf = (ctypes.c_ulonglong * K)()
+        assert s.lib.wbq_diag_stamps(s.ctx, buf, 1) == 0
+        st = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+        tau, status, iters = s.outputs()
+        rep = st[12] > st[8]
+        row = {"tick": t, "us": 1e3 * ms, "status": int(status[0]), "iters": int(iters[0]), "repair": bool(rep),
+               "fast_cycles": int(st[5] - st[0])}
+        if rep:
+            row.update({"gj": int(st[9] - st[8]), "bvls": int(st[10] - st[9]), "pins_eq": int(st[11] - st[10]),
+                        "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14])})
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    s.close()
+    json.dump(rows, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -100,3 +100,24 @@ def test_forceacc_dummy_driver_matches_oracle(tmp_path, oracle_lib):
     ok = st_r == 0
     assert ok.sum() >= len(ok) - 2
     assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, rel_err(d["tau"][ok], tau_r[ok])
+
+
+@pytest.mark.parametrize("plugin", ["qppvm", "forceacc"])
+def test_plugin_storage_order_independent(tmp_path, plugin):
+    """The shells copy Jacobians and M element by element into the ABI's row-major layout, so
+    the applied torques are bit-identical with a column-major (Eigen's default) and a row-major
+    compat MatrixXd."""
+    from qppvm_amd import build
+    build.build_plugins()
+    outs = []
+    for drv in (build.DRIVER, build.DRIVER_RM):
+        dump = str(tmp_path / (os.path.basename(drv) + ".bin"))
+        args = [drv, "--ticks", "60", "--dump", dump, "30"]
+        if plugin == "forceacc":
+            args[1:1] = ["--plugin", "forceacc"]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        if plugin == "forceacc":
+            assert '"sync_flags": 5' in r.stdout  # Sync::Position | Sync::Effort (ForceAcc.cpp:242)
+        outs.append(open(dump, "rb").read())
+    assert outs[0] == outs[1]

@@ -56,3 +56,23 @@ def test_gloo_sharded_solve_matches_single_process(tmp_path, oracle_lib, world, 
     np.testing.assert_array_equal(got["st"], st)
     np.testing.assert_array_equal(got["tiny"], np.zeros((1, 2)))
     np.testing.assert_array_equal(got["mx"], [world - 0.5, 0.0])
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N relaunches itself as N ranks only when N GPUs are visible; otherwise it
+    exits non-zero with a clear message before touching any GPU."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "64", "--no-pmc"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "--gpus 64 requested but only" in r.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    import subprocess
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--no-pmc"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
