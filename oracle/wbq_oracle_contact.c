@@ -215,6 +215,21 @@ int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const doubl
             --k;
         }
     }
+    if (status == WBQ_REF_OK) {
+        /* the incremental x must meet every row: a degenerate active set whose steps drifted is a
+         * numerical failure, never a silent success */
+        for (int j = 0; j < me && status == WBQ_REF_OK; ++j) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) s += E[(size_t)j * n + i] * x[i];
+            if (fabs(s - e[j]) > 1e-8 * cmaxd(1.0, cmaxd(fabs(s), fabs(e[j])))) status = WBQ_REF_NUMERICAL;
+        }
+        for (int j = 0; j < mi && status == WBQ_REF_OK; ++j) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) s += C[(size_t)j * n + i] * x[i];
+            const double sc = 1e-8 * cmaxd(1.0, cmaxd(fabs(s), cmaxd(fabs(clo[j]), fabs(chi[j]))));
+            if (clo[j] - s > sc || s - chi[j] > sc) status = WBQ_REF_NUMERICAL;
+        }
+    }
 out:
     if (iters) *iters = it;
     free(A);

@@ -36,11 +36,16 @@
 #include "wbq_kernels.h"
 #include "wbq_device.h"
 #include "dual_gi.h"
+#include "qppvm_repair.h"
 
 #include <type_traits>
 
 namespace wbq {
 namespace {
+
+// Grid of the level-0 repair kernel (grid-stride over its work list; a solve with nothing to
+// repair costs one near-empty launch of this many blocks)
+constexpr unsigned kContactRepairGrid = 256;
 
 // Per-instance LDS layout in doubles. Compact constraint index ci (= GI lane):
 //   ci <  NJ             joint row a = ci (a < 6: dynamic feasibility, an equality;
@@ -233,15 +238,139 @@ struct ContactGi {
 // compact index of equality a (a < 6: dynamic feasibility rows, then the waist rows)
 __device__ __forceinline__ int eq_row(int a, int NJ) { return a < 6 ? a : NJ + a - 6; }
 
-template <int NQ, bool TR, int KMR>
-__global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel(const ContactArgs a)
+// Level 0 of the contact form when the waist task cannot be met at b_w (ForceAcc.cpp:131-137,189:
+// QPOases_sot solves waist / (postural + feet), so level 1 keeps the waist at its level-0 optimum
+// y0*). With tau = M qdd + h - sum_c J_c^T [f_c; 0], dynamic feasibility is tau_fb = 0 and every
+// other row is a box in z = (tau_a, f): qdd = M^-1 (S_a^T tau_a - h + J_c,lin^T f), so level 0 is
+//   min 0.5 ||A0 z - (b_w + W^T h)||^2,  lo_z <= z <= hi_z,   W = M^-1 J_w^T,
+//   A0 columns: tau_a -> row a of W;  f_ck -> W^T J_c[k]^T
+// (without torque rows tau_a is unbounded). BVLS (the QPPVM level-0 repair's, qppvm_repair.h)
+// gives z*; y0* = A0 z* - W^T h becomes the waist rows' target, and every variable the level-0
+// gradient w = A0^T (b - A0 z*) holds at a bound is pinned there (its torque or force row becomes an
+// equality), as oracle/wbq_oracle.c:wbq_ref_qppvm_one pins for the QPPVM form. The oracle
+// (oracle/wbq_oracle_contact.c:wbq_ref_contact_one) reaches y0* through a 1e-10 ridge instead:
+// the same optimum, to the ridge. Lane roles: joint lane i < n for W; variable lane
+// j < n - 6 = tau_{6+j}, then the 3 nc forces; constraint lane ci for the targets and the pins.
+// The waist rows and the pins are dependent on the level-0 face: y - y0* = A0 (z - z*) moves only
+// along the unpinned columns, so only a pivot basis of their span (wkeep: a mask of waist rows,
+// from a pivoted Cholesky of their Gram) is kept as level-1 rows -- the others are implied, and
+// keeping them makes the final active set exactly singular.
+// Updates this lane's row limits (lo, hi); returns the BVLS iterations, capped = BVLS hit its cap.
+template <int NQ>
+__device__ int contact_level0(const ContactArgs &a, long b, double *S, const ContactLayout &L, int i, double h_i,
+                              double &lo, double &hi, bool &capped, int &wkeep)
+{
+    const int n = a.n, nc = a.nc, nf = 3 * nc, na = n - 6;
+    const bool qrow = i < n;
+    const int ic = qrow ? i : n - 1;
+    const long B = a.B;
+    // W = M^-1 J_w^T, lane i holding row i: block Gauss-Jordan on M's rows (re-read: L2) with the
+    // J_w columns as right-hand sides; the pivot panel in the T region (not written yet)
+    double A[NQ], w[6];
+    {
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
+        const __amdgpu_buffer_rsrc_t Wrs = rsrc_at(a.Jw, b, B, 6L * n);
+#pragma unroll
+        for (int r = 0; r < NQ; ++r) A[r] = bload(Mrs, (int)(8 * ic), 8 * (r < n ? r : n - 1) * n);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) w[r] = bload(Wrs, (int)(8 * ic), 8 * r * n);
+#pragma unroll
+        for (int r = 0; r < NQ; ++r) A[r] = (qrow && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) w[r] = qrow ? w[r] : 0.0;
+    }
+    __syncthreads();
+    (void)block_gj<NQ, 6, 6>(A, w, n, i, S + L.PN, S + L.RH);
+    // b = b_w + W^T h (the waist targets are the waist rows' limits)
+    double bv[6], hw[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        hw[r] = isum<64>(qrow ? w[r] * h_i : 0.0);
+        bv[r] = __shfl(lo, L.NJ + r) + hw[r];
+    }
+    // the columns of A0 on the variable lanes
+    const bool tvar = i < na, fvar = i >= na && i < na + nf;
+    const int f = fvar ? i - na : 0;
+    double acol[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) acol[r] = __shfl(w[r], tvar ? 6 + i : 0);
+    {
+        const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
+        for (int ff = 0; ff < nf; ++ff) {
+            const int c = ff / 3, k = ff - 3 * c;
+            const double jv = bload(Jrs, (int)(8 * ic), 8 * (6 * c + k) * n);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const double v = isum<64>(qrow ? w[r] * jv : 0.0);
+                if (fvar && f == ff) acol[r] = v;
+            }
+        }
+    }
+    double zlo = 0.0, zhi = 0.0;
+    if (tvar) {
+        zlo = a.torque_rows ? a.tau_min[6 + i] : -kInf;
+        zhi = a.torque_rows ? a.tau_max[6 + i] : kInf;
+    } else if (fvar) {
+        const int k = f % 3;
+        const bool on = (a.cmask[b] >> (f / 3)) & 1;
+        const double fl = k == 0 ? a.f_lb[0] : (k == 1 ? a.f_lb[1] : a.f_lb[2]);
+        const double fu = k == 0 ? a.f_ub[0] : (k == 1 ? a.f_ub[1] : a.f_ub[2]);
+        zlo = on ? fl : 0.0; // an inactive contact's forces are fixed at zero
+        zhi = on ? fu : 0.0;
+    }
+    const bool row = tvar || fvar;
+    const BvlsOut bz = bvls<64, 6>(acol, bv, 6, zlo, zhi, row, true, 0, 50 * (na + nf) + 100);
+    double ys[6], abm = 0.0, g = 0.0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ys[r] = isum<64>(row ? acol[r] * bz.xv : 0.0);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        abm = fma(acol[r], bv[r], abm);
+        g = fma(acol[r], bv[r] - ys[r], g);
+    }
+    abm = fmax(1.0, imax<64>(row ? fabs(abm) : 0.0));
+    const int pin = (row && g > 1e-9 * abm) ? 1 : ((row && g < -1e-9 * abm) ? -1 : 0);
+    {
+        constexpr int NT = 21;
+        const bool mov = row && pin == 0 && zlo != zhi; // columns y can still move along
+        double gu[NT];
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+            for (int c = 0; c <= p; ++c) gu[tri(p, c)] = mov ? acol[p] * acol[c] : 0.0;
+        isum_vec<64, NT>(gu);
+        PivChol<6> pc;
+        pc.factor(gu, 6, 1e-10);
+        wkeep = 0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wkeep |= (c < pc.k) ? (1 << pc.piv[c]) : 0;
+    }
+    // constraint lanes: torque row a <-> variable a - 6, force row <-> variable na + its force
+    const int ci = i;
+    const bool trow = ci >= 6 && ci < L.NJ, frow = ci >= L.NJ + 6 && ci < L.ME;
+    const int pin_c = __shfl(pin, trow ? ci - 6 : (frow ? na + ci - L.NJ - 6 : 0));
+    if ((trow || frow) && pin_c > 0) lo = hi; // held at the upper limit
+    if ((trow || frow) && pin_c < 0) hi = lo; // held at the lower limit
+    if (ci >= L.NJ && ci < L.NJ + 6) {
+        double y = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) y = (ci - L.NJ == r) ? ys[r] - hw[r] : y;
+        lo = hi = y; // the waist rows keep the level-0 optimum y0*
+    }
+    capped = bz.capped;
+    return bz.it;
+}
+
+// The whole solve of instance b by one wave (lane i = threadIdx.x). REPAIR (the follow-up
+// kernel): level 0 first (contact_level0: BVLS for y0*, pins), then level 1 with those targets.
+template <int NQ, bool TR, int KMR, bool REPAIR>
+__device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b)
 {
     constexpr int NRC = TR ? 40 : 16; // Gauss-Jordan right-hand sides per pass
     extern __shared__ __attribute__((aligned(16))) double S[];
     const int n = a.n, nc = a.nc, nf = 3 * nc;
     const ContactLayout L(n, nc, TR, NQ, NRC);
     const int i = threadIdx.x;
-    const long b = blockIdx.x;
     const int cm = a.cmask[b];
     const bool qrow = i < n;
     const int ic = qrow ? i : n - 1;
@@ -446,6 +575,16 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
     __syncthreads();
     if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
     WBQ_STAMP(4);
+    int it0 = 0;
+    bool l0cap = false;
+    int wkeep = 0x3f; // waist rows kept as level-1 rows (all, except after a level-0 repair)
+    const double lo_free = lo, hi_free = hi, s_x0 = s_i; // (a repair retry restarts from these)
+    const int kind_free = kind;
+    (void)kind_free;
+    if constexpr (REPAIR) { // level 0 not attainable at b_w: y0* and the pins first
+        if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ>(a, b, S, L, i, h_i, lo, hi, l0cap, wkeep);
+        __syncthreads();
+    }
 
     // ------------------------------------ 6. dual active set in constraint space
     // Slot a (lane a < k) = a-th active row: act (compact row), sgn (normal = sgn * a_act),
@@ -464,23 +603,55 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         Tcol.bind(S + L.TT + (i < L.NX ? i : 0), L.TS);
         GA.bind(S + L.GM + (ci < ME ? ci : 0) * L.GS, S + L.AC);
     }
+    GiState gs; // slots: act = compact row
+    // the repair kernel's level 1: the pinned rows and the waist at y0* are exactly dependent on the
+    // level-0 face; if that solve fails numerically (status 1 or 3) it runs once more without the
+    // pins (the waist rows at y0* alone keep level 1 on the face)
+    constexpr int kAttempts = REPAIR ? 2 : 1;
+#pragma unroll 1
+    for (int attempt = 0; attempt < kAttempts; ++attempt) {
+    if (attempt > 0) {
+        if (ci < NJ || ci >= NJ + 6) {
+            lo = lo_free;
+            hi = hi_free;
+        }
+        wkeep = 0x3f;
+        s_i = s_x0;
+        __syncthreads();
+    }
+    if constexpr (REPAIR) kind = (ci >= NJ && ci < NJ + 6 && !((wkeep >> (ci - NJ)) & 1)) ? 0 : kind_free;
+    // batch row c: the dynamic-feasibility rows, then the kept waist rows; nb of them (12 but
+    // after a repair)
+    const int nb = REPAIR ? 6 + __popc((unsigned)wkeep) : 12;
+    auto brow = [&](int c) {
+        if constexpr (!REPAIR) {
+            return eq_row(c, NJ);
+        } else {
+            if (c < 6) return c;
+            unsigned m = (unsigned)wkeep;
+            for (int j = 6; j < c && j < 12; ++j) m &= m - 1;
+            return m ? NJ + __builtin_ctz(m) : NJ;
+        }
+    };
     Trow.zero_from(0);
     Tcol.zero_from(0);
     GA.zero_from(0);
-    GiState gs; // slots: act = compact row
-    gs.status = notspd ? 3 : (a.limits_crossed ? 2 : 0);
+    gs = GiState();
+    gs.status = notspd ? 3 : (a.limits_crossed ? 2 : (l0cap ? 1 : 0));
     if (gs.status == 0) {
         // The 12 equality rows in one batch. Lane r < 12 holds row r of Gamma_EE; a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane
         // c then forward-substitutes column c of T = L^-1 against the broadcast rows of L, and
         // lambda_E = T^T T (e_E - s_E), s += Gamma[:, E] lambda_E.
-        const int er = eq_row(i < 12 ? i : 0, NJ);
+        // (rows past nb: identity, decoupled, never active)
+        const int er = brow(i < nb ? i : 0);
         double g[12];
 #pragma unroll
-        for (int c = 0; c < 12; ++c) g[c] = (i < 12) ? S[L.GM + er * L.GS + eq_row(c, NJ)] : 0.0;
+        for (int c = 0; c < 12; ++c)
+            g[c] = (i < nb && c < nb) ? S[L.GM + er * L.GS + brow(c)] : ((i == c && i < 12) ? 1.0 : 0.0);
         double gd = 0.0;
 #pragma unroll
-        for (int c = 0; c < 12; ++c) gd = (i == c) ? g[c] : gd;
+        for (int c = 0; c < 12; ++c) gd = (i == c && i < nb) ? g[c] : gd;
         const double dmx = imax<64>(gd);
         bool sing = false;
 #pragma unroll
@@ -508,31 +679,32 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         // of the TT region: the LDS Trow itself, or scratch for the register Trow)
 #pragma unroll
         for (int r = 0; r < 12; ++r) {
-            Tcol.put(r, i < 12, t[r]);
-            if (i < 12) S[L.TT + r * L.TS + i] = t[r];
+            const double tr = (i < nb && r < nb) ? t[r] : 0.0;
+            Tcol.put(r, i < 12, tr);
+            if (i < 12) S[L.TT + r * L.TS + i] = tr;
         }
         const double ye = __shfl(lo - s_i, er); // e_E - s_E (every lane active: sources up to lane NJ + 5)
-        if (i < 12) S[L.VV + i] = ye;
-        S[L.AC + i] = (double)er; // slots 0..11 (the gathered Gamma columns of the LDS variant)
+        if (i < 12) S[L.VV + i] = i < nb ? ye : 0.0;
+        S[L.AC + i] = (double)er; // slots 0..nb-1 (the gathered Gamma columns of the LDS variant)
         __syncthreads();
-        if constexpr (SREG) Trow.load_if(i < 12, S + L.TT + (i < 12 ? i : 0) * L.TS, 12);
-        const double w = i < 12 ? Trow.dot(S + L.VV, 12) : 0.0;
+        if constexpr (SREG) Trow.load_if(i < nb, S + L.TT + (i < nb ? i : 0) * L.TS, nb);
+        const double w = i < nb ? Trow.dot(S + L.VV, nb) : 0.0;
         S[L.LV + i] = w;
         __syncthreads();
-        const double lm = i < 12 ? Tcol.dot(S + L.LV, 12) : 0.0; // lambda_E
+        const double lm = i < nb ? Tcol.dot(S + L.LV, nb) : 0.0; // lambda_E
         S[L.RV + i] = lm;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 12; ++q)
-            GA.put(q, kind != 0, kind != 0 ? S[L.GM + ci * L.GS + eq_row(q, NJ)] : 0.0);
-        if (kind != 0) s_i += GA.dot(S + L.RV, 12);
-        if (i < 12) {
+            GA.put(q, kind != 0, (kind != 0 && q < nb) ? S[L.GM + ci * L.GS + brow(q)] : 0.0);
+        if (kind != 0) s_i += GA.dot(S + L.RV, nb);
+        if (i < nb) {
             gs.act = er;
             gs.aeq = true;
             gs.lam = lm;
         }
-        gs.onact = ci < 6 || (ci >= NJ && ci < NJ + 6);
-        gs.k = 12;
+        gs.onact = ci < 6 || (ci >= NJ && ci < NJ + 6 && (!REPAIR || ((wkeep >> (ci - NJ)) & 1)));
+        gs.k = nb;
         gs.iters = 1;
         if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
         __syncthreads();
@@ -550,8 +722,22 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
         dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }
+    if (gs.status != 1 && gs.status != 3) break;
+    }
     int status = gs.status;
-    const int iters = gs.iters;
+    const int iters = gs.iters + it0;
+    if constexpr (!REPAIR) {
+        // no step exists: the waist task is not attainable at b_w (the rows are boxes in
+        // (tau_a, f), so nothing else can be infeasible) -- the repair kernel solves level 0 first
+        if (status == 2 && !a.limits_crossed && a.wl) {
+            if (i == 0) {
+                a.status[b] = -2;
+                const int idx = atomicAdd(&a.work[a.epoch * 2 + 1], 1);
+                a.wl[idx] = (int)b;
+            }
+            return;
+        }
+    }
 
     // ------------------------------------------------------------------ 7. outputs
     __syncthreads();
@@ -595,7 +781,29 @@ __global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel
 }
 
 template <int NQ, bool TR, int KMR>
-hipError_t launch_t(const ContactArgs &a, hipStream_t stream)
+__global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel(const ContactArgs a)
+{
+    contact_solve<NQ, TR, KMR, false>(a, (long)blockIdx.x);
+}
+
+// Level-0 repair: the instances contact_kernel listed (status -2), grid-stride; its own register
+// budget (the BVLS of the level-0 step) leaves the main kernel's alone.
+template <int NQ, bool TR, int KMR>
+__global__ __launch_bounds__(64, 1) void contact_repair_kernel(const ContactArgs a)
+{
+    const int cnt = a.work[a.epoch * 2 + 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's counter (its parity was last used
+        a.work[(a.epoch ^ 1) * 2] = 0;         // by the previous solve, which has completed)
+        a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+    }
+    for (long e = blockIdx.x; e < cnt; e += gridDim.x) {
+        __syncthreads(); // the previous instance's LDS is dead
+        contact_solve<NQ, TR, KMR, true>(a, uniform_long(a.wl[e]));
+    }
+}
+
+template <int NQ, bool TR, int KMR>
+hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     constexpr int NRC = TR ? 40 : 16;
     const ContactLayout L(a.n, a.nc, TR, NQ, NRC);
@@ -605,14 +813,24 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream)
     const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR>, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    hipError_t e2 = hipGetLastError();
+    if (e2 != hipSuccess || !a.wl) return e2;
+    if (mid) {
+        e2 = hipEventRecord(mid, stream);
+        if (e2 != hipSuccess) return e2;
+    }
+    e2 = ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR>, lds);
+    if (e2 != hipSuccess) return e2;
+    const unsigned grid = a.B < (int)kContactRepairGrid ? (unsigned)a.B : kContactRepairGrid;
+    hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR>), dim3(grid), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 
 template <int NQ>
-hipError_t launch_nq(const ContactArgs &a, hipStream_t stream)
+hipError_t launch_nq(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {
-    if (a.torque_rows) return launch_t<NQ, true, 64>(a, stream);
-    return a.nc <= 2 ? launch_t<NQ, false, 18>(a, stream) : launch_t<NQ, false, 24>(a, stream);
+    if (a.torque_rows) return launch_t<NQ, true, 64>(a, stream, mid);
+    return a.nc <= 2 ? launch_t<NQ, false, 18>(a, stream, mid) : launch_t<NQ, false, 24>(a, stream, mid);
 }
 
 }  // namespace
@@ -624,10 +842,10 @@ size_t contact_lds_bytes(int n, int nc, int torque_rows)
     return sizeof(double) * ContactLayout(n, nc, tr, NQ, tr ? 40 : 16).SIZE;
 }
 
-hipError_t launch_contact(const ContactArgs &a, hipStream_t stream)
+hipError_t launch_contact(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     if (a.B <= 0) return hipSuccess;
-    return a.n <= 32 ? launch_nq<32>(a, stream) : launch_nq<64>(a, stream);
+    return a.n <= 32 ? launch_nq<32>(a, stream, mid) : launch_nq<64>(a, stream, mid);
 }
 
 }  // namespace wbq

@@ -6,8 +6,8 @@
 // active-set Gram Gamma_AA = L L^T is kept as T = L^-1 (an add appends one row of T in
 // closed form, a drop re-appends the rows after it) and x is rebuilt from the multipliers,
 // x = x0 + H^-1 A_A^T lambda, only when the active set settles; two steps of iterative
-// refinement on the final active set (residuals exact in x-space) and a re-check of every
-// row follow (the algorithm the oracle restates in
+// refinement on the final active set (residuals exact in x-space; up to four while an active row
+// still misses, for nearly dependent sets) and a re-check of every row follow (the algorithm the oracle restates in
 // oracle/wbq_oracle_contact.c and oracle/wbq_oracle.c).
 //
 // The problem supplies a policy P with
@@ -47,6 +47,13 @@ struct SlotVec<KM, true> {
         for (int j = 0; j < KM; ++j) v[j] = cond ? 0.0 : v[j];
     }
     __device__ void put(int c, bool cond, double x) { v[c] = cond ? x : v[c]; } // c static after unrolling
+    __device__ double get(int c) const
+    {
+        double r = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) r = (j == c) ? v[j] : r;
+        return r;
+    }
     __device__ void put_dyn(int c, bool cond, double x)
     {
 #pragma unroll
@@ -99,6 +106,7 @@ struct SlotVec<KM, false> {
     {
         if (cond) p[c] = x;
     }
+    __device__ double get(int c) const { return p[c]; }
     __device__ void put_dyn(int c, bool cond, double x)
     {
         if (cond) p[c] = x;
@@ -202,6 +210,8 @@ struct GAView {
 };
 
 constexpr int kGiRounds = 8; // x rebuilds (each followed by a re-check of every row)
+constexpr int kGiPasses = 5; // per rebuild: x from the multipliers, then up to 4 refinement passes
+constexpr double kDropPivot = 1e-9; // relative pivot below which a slot is dropped when a rebuild misses
 
 // LDS scratch vectors of the loop (72 doubles each: slot dots read 8 past the active count)
 struct GiVecs {
@@ -226,12 +236,52 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                                         GAT &GA, int kind, double lo, double hi, double nrm, double &s_i, GiState &g,
                                         int maxit)
 {
-    bool need_select = true, dirty = true;
+    bool need_select = true, dirty = true, recheck = false;
     int cp = 0;
     double sgp = 1.0, bnd = 0.0, lamp = 0.0;
     bool peq = false;
     bool go = g.status == 0;
+    int drop = -1; // slot to remove at the top of the next pass (uniform)
     while (go) {
+        if (drop >= 0) {
+            // remove slot drop from the active set: the slots after it move down, the rows and
+            // columns of T before it stand and the ones after it are re-appended
+            const int cb = __shfl(g.act, drop);
+            if (i == cb) g.onact = false;
+            const int na = __shfl(g.act, i + 1);
+            const double ns = __shfl(g.sgn, i + 1), nl = __shfl(g.lam, i + 1);
+            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1) != 0;
+            if (i >= drop) {
+                g.act = na;
+                g.sgn = ns;
+                g.lam = nl;
+                g.aeq = ne;
+            }
+            GA.shift_down(drop, g.k);
+            --g.k;
+            Trow.zero_if(i >= drop);
+            Tcol.zero_from(drop);
+            __syncthreads();
+            for (int a2 = drop; a2 < g.k; ++a2) {
+                const int cq = __shfl(g.act, a2);
+                const double sq = __shfl(g.sgn, a2);
+                S[V.VV + i] = i < a2 ? g.sgn * sq * pb.gamma(g.act, cq) : 0.0;
+                __syncthreads();
+                const double l2 = i < a2 ? Trow.dot(S + V.VV, a2) : 0.0;
+                S[V.LV + i] = l2;
+                __syncthreads();
+                const double r2 = i < a2 ? Tcol.dot(S + V.LV, a2) : 0.0;
+                const double e2 = pb.gamma(cq, cq) - isum<64>(l2 * l2);
+                const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
+                const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
+                Tcol.put_dyn(a2, i <= a2, tk2);
+                S[V.WV + i] = tk2;
+                __syncthreads();
+                Trow.load_if(i == a2, S + V.WV, a2 + 1);
+                __syncthreads();
+            }
+            drop = -1;
+        }
         if (need_select) {
             double v = -1.0;
             if (kind == 2 && !g.onact) {
@@ -241,7 +291,8 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             }
             int pi = i;
             iargmax<64>(v, pi);
-            if (!(v > 0.0)) {
+            if (!(v > 0.0) || recheck) {
+                recheck = false;
                 // no violated row: x is current unless steps were taken since the last
                 // rebuild; otherwise rebuild x from the multipliers, refine (x, lambda) on the
                 // active set, and re-check every row with the exact activities. A re-check
@@ -258,7 +309,8 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 S[V.RV + i] = i < g.k ? g.sgn * g.lam : 0.0;
                 S[V.AC + i] = (double)g.act;
                 __syncthreads();
-                for (int pass = 0; pass < 3; ++pass) {
+#pragma unroll 1
+                for (int pass = 0; pass < kGiPasses; ++pass) {
                     if (pass > 0) {
                         // residual of the active rows, exact in x-space; correction through T
                         double a_act;
@@ -269,6 +321,9 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                             a_act = i < g.k ? pb.activity(g.act) : 0.0;
                         }
                         const double res = i < g.k ? g.sgn * ((g.sgn > 0.0 ? lo_a : hi_a) - a_act) : 0.0;
+                        // two refinement passes always; more only while an active row still misses:
+                        // a nearly dependent active set gains ~eps cond(Gamma_AA) per pass
+                        if (pass > 2 && imax<64>(i < g.k ? fabs(res) / (1.0 + fabs(a_act)) : 0.0) <= 1e-13) break;
                         S[V.VV + i] = res;
                         __syncthreads();
                         const double y = Trow.dot(S + V.VV, g.k);
@@ -287,6 +342,21 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 // of a nearly dependent active set) is garbage and so is x: fail loudly
                 const double miss = (kind != 0 && g.onact) ? fmin(fabs(s_i - lo), fabs(s_i - hi)) / (1.0 + fabs(s_i)) : 0.0;
                 if (imax<64>(miss) > 1e-8) {
+                    // a nearly dependent row added by the loop: drop the slot with the smallest
+                    // relative pivot d^2 / Gamma_pp = 1 / (T_aa^2 Gamma_pp) -- an implied row, which
+                    // the exact activities of the next rebuild still meet -- and rebuild; the
+                    // rounds cap bounds this. No such slot: fail (status 3)
+                    const double tdi = Trow.get(i);
+                    const int ka = __shfl(kind, g.act);
+                    double pv = (i < g.k && ka == 2) ? 1.0 / (tdi * tdi * pb.gamma(g.act, g.act)) : kInf;
+                    int blk = i;
+                    iargmin<64>(pv, blk);
+                    if (pv < kDropPivot) {
+                        drop = blk;
+                        dirty = true;
+                        recheck = true;
+                        continue;
+                    }
                     g.status = 3;
                     break;
                 }
@@ -303,7 +373,6 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             g.status = 1;
             break;
         }
-        dirty = true;
         // ---- step for row cp: r = Gamma_AA^-1 v, ds = A z (change of every activity)
         const double gpp = pb.gamma(cp, cp);
         S[V.VV + i] = i < g.k ? g.sgn * sgp * pb.gamma(g.act, cp) : 0.0;
@@ -331,13 +400,23 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
         // and with k = dim active rows the set spans the primal space: cp is dependent
         const double t2 = (g.k < pb.dim && zz > P::kDep * gpp) ? -slack / zz : kInf;
         if (t1 >= kInf && t2 >= kInf) {
-            g.status = 2; // no step: the rows cannot all be met
+            // no step: the rows cannot all be met -- unless the incremental activities drifted
+            // since the last exact rebuild; then rebuild x, re-check every row exactly and select
+            // again (the row's partial multiplier is dropped with the rebuild), and report 2 only
+            // when the exact activities still leave no step
+            if (dirty) {
+                recheck = true;
+                need_select = true;
+                continue;
+            }
+            g.status = 2;
             break;
         }
         if (t2 <= t1 && g.k >= KM) { // cannot happen for independent rows; guard the storage
             g.status = 3;
             break;
         }
+        dirty = true; // a step is taken: the incremental activities drift from the exact ones
         const double t = fmin(t1, t2);
         s_i = fma(t, ds, s_i);
         if (i < g.k) g.lam = fma(-t, r, g.lam);
@@ -361,41 +440,7 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             need_select = true;
             __syncthreads();
         } else { // drop slot blk (its multiplier reached zero), keep stepping on cp
-            const int cb = __shfl(g.act, blk);
-            if (i == cb) g.onact = false;
-            const int na = __shfl(g.act, i + 1);
-            const double ns = __shfl(g.sgn, i + 1), nl = __shfl(g.lam, i + 1);
-            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1) != 0;
-            if (i >= blk) {
-                g.act = na;
-                g.sgn = ns;
-                g.lam = nl;
-                g.aeq = ne;
-            }
-            GA.shift_down(blk, g.k);
-            --g.k;
-            // rows and columns of T before blk stand; re-append the slots after it
-            Trow.zero_if(i >= blk);
-            Tcol.zero_from(blk);
-            __syncthreads();
-            for (int a2 = blk; a2 < g.k; ++a2) {
-                const int cq = __shfl(g.act, a2);
-                const double sq = __shfl(g.sgn, a2);
-                S[V.VV + i] = i < a2 ? g.sgn * sq * pb.gamma(g.act, cq) : 0.0;
-                __syncthreads();
-                const double l2 = i < a2 ? Trow.dot(S + V.VV, a2) : 0.0;
-                S[V.LV + i] = l2;
-                __syncthreads();
-                const double r2 = i < a2 ? Tcol.dot(S + V.LV, a2) : 0.0;
-                const double e2 = pb.gamma(cq, cq) - isum<64>(l2 * l2);
-                const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
-                const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
-                Tcol.put_dyn(a2, i <= a2, tk2);
-                S[V.WV + i] = tk2;
-                __syncthreads();
-                Trow.load_if(i == a2, S + V.WV, a2 + 1);
-                __syncthreads();
-            }
+            drop = blk;
             need_select = false;
         }
     }

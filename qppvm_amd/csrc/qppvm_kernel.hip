@@ -352,7 +352,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
 // active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. Rare path:
 // kept out of the other kernels so that its registers do not weigh on them.
 template <int NP, int M0>
-__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_repair_kernel(const QppvmArgs a)
+__global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];

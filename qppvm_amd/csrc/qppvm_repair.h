@@ -235,66 +235,30 @@ __device__ __forceinline__ void isum_vec(double (&v)[K])
         for (int c = 0; c < K; ++c) v[c] += __shfl_xor(v[c], m, NP);
 }
 
-struct RepairOut {
-    double lo, hi, u; // (possibly pinned) limits and the new u of this lane
-    int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
-    bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
+// BVLS (Stark-Parker; the algorithm of oracle/wbq_oracle.c:wbq_ref_level0) on
+//   min 0.5 ||A z - b||^2  s.t.  lo <= z <= hi
+// with lane i owning variable z_i and its column acol (rows c < m0 of the M0 slots) and every lane
+// holding b; padding lanes have row = false (never free). active = this instance runs (lanes of an
+// instance agree); st0 = the start state of the lane (0 free, -1 at lo, +1 at hi: a warm start,
+// any state is valid). Returns the lane's z_i, its final state, the iterations and whether the
+// iteration cap ended it.
+struct BvlsOut {
+    double xv;
+    int st, it;
+    bool capped;
 };
-
-// Level-0 repair for the instances with rep set (every lane of the wave calls this; the
-// instance -> lane mapping is the kernel's). Level 0 in x-space is
-//   min 0.5 ||A0 x - b0||^2  s.t. lo <= x <= hi,   A0 = G M^-1   (QPPVMPlugin.cpp:129-152,177)
-// Solved by BVLS (Stark-Parker), the algorithm of oracle/wbq_oracle.c:wbq_ref_level0, with
-// lane i owning column a_i = (M^-1 G^T)_i (block Gauss-Jordan on the M rows, reloaded from
-// HBM/L2: this path is rare). Then y* = A0 x*, every variable the level-0 gradient
-// w = A0^T (b0 - y*) holds at a bound is pinned there (lo = hi, as wbq_ref_qppvm_one does),
-// and u is reset to the least-distance point of G u = y*, with the Q1 rows (orthonormal
-// basis of range(G^T), zero rows past its rank) in LDS for a fresh dual active set.
-// Not inlined: its registers do not weigh on the active-set loop.
 template <int NP, int M0>
-__device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff, long b, int i, bool rep, double lo,
-                                                double hi, bool warm)
+__device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (&b0v)[M0], int m0, double lo,
+                                        double hi, bool row, bool active, int st0, int maxit)
 {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    double *S = smem + soff;
-    constexpr int RS = NP + 1;
     constexpr int NT = M0 * (M0 + 1) / 2;
-    const ActiveLayout<NP> L(a.ntasks, a.m0);
-    const int n = a.n, m0 = a.m0;
-    const int ic = i < n ? i : n - 1;
-    const bool row = rep && i < n;
-    RepairOut out{lo, hi, 0.0, 0, 0, false};
-    double gcol[M0], acol[M0], b0v[M0];
-    const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
-#pragma unroll
-    for (int c = 0; c < M0; ++c) {
-        const bool on = rep && c < m0;
-        const int rr = on ? a.row_sel[c] : 0;
-        gcol[c] = (on && row) ? a.J[(b * a.ntasks * 6 + rr) * n + ic] : 0.0;
-        b0v[c] = on ? a.b0_scr[b * kM0Max + c] : 0.0;
-        acol[c] = gcol[c];
-    }
-    // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
-    // are rebuilt below)
-    {
-        // 64-bit addressing: the instances of a wave come from a work list (no uniform base)
-        const double *Mb = a.M + b * n * n + ic;
-        double A[NP];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
-        __syncthreads();
-        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
-    }
-    WBQ_STAMP(9);
-    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0)
+    const int i = threadIdx.x & (NP - 1); // lane within the instance
+    BvlsOut out{0.0, 0, 0, false};
     double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
     int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
-    if (row && warm) {    // warm start: the bound state of the last repair (any state is valid)
-        const int w = a.ws_state[b * NP + i];
-        st = (w < 0) ? -1 : (w > 0 ? 1 : 0);
-        xv = st < 0 ? lo : (st > 0 ? hi : xv);
+    if (row && st0 != 0) {
+        st = st0 < 0 ? -1 : 1;
+        xv = st < 0 ? lo : hi;
     }
     if (row && lo == hi) {
         st = -1;
@@ -306,10 +270,8 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
     const double wtb = fabs(abm);
     abm = fmax(1.0, imax<NP>(wtb));
-    const double pintol = 1e-9 * abm;
     int freed = -1, it = 0;
-    const int maxit = 50 * n + 100;
-    bool outer = rep;
+    bool outer = active;
     while (__any(outer)) {
         bool inner = outer;
         while (__any(inner)) {
@@ -404,7 +366,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
             if (!(v > wtol)) {
                 outer = false;
             } else if (it >= maxit) {
-                out.status = 1;
+                out.capped = true;
                 outer = false;
             } else {
                 if (i == best) st = 0; // exclusions persist until the inner loop makes progress
@@ -412,6 +374,81 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
             }
         }
     }
+    out.xv = xv;
+    out.st = st;
+    out.it = it;
+    return out;
+}
+
+struct RepairOut {
+    double lo, hi, u; // (possibly pinned) limits and the new u of this lane
+    int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
+    bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
+};
+
+// Level-0 repair for the instances with rep set (every lane of the wave calls this; the
+// instance -> lane mapping is the kernel's). Level 0 in x-space is
+//   min 0.5 ||A0 x - b0||^2  s.t. lo <= x <= hi,   A0 = G M^-1   (QPPVMPlugin.cpp:129-152,177)
+// Solved by BVLS (Stark-Parker), the algorithm of oracle/wbq_oracle.c:wbq_ref_level0, with
+// lane i owning column a_i = (M^-1 G^T)_i (block Gauss-Jordan on the M rows, reloaded from
+// HBM/L2: this path is rare). Then y* = A0 x*, every variable the level-0 gradient
+// w = A0^T (b0 - y*) holds at a bound is pinned there (lo = hi, as wbq_ref_qppvm_one does),
+// and u is reset to the least-distance point of G u = y*, with the Q1 rows (orthonormal
+// basis of range(G^T), zero rows past its rank) in LDS for a fresh dual active set.
+// Not inlined: its registers do not weigh on the active-set loop.
+template <int NP, int M0>
+__device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff, long b, int i, bool rep, double lo,
+                                                double hi, bool warm)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double *S = smem + soff;
+    constexpr int RS = NP + 1;
+    constexpr int NT = M0 * (M0 + 1) / 2;
+    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const int n = a.n, m0 = a.m0;
+    const int ic = i < n ? i : n - 1;
+    const bool row = rep && i < n;
+    RepairOut out{lo, hi, 0.0, 0, 0, false};
+    double gcol[M0], acol[M0], b0v[M0];
+    const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        const bool on = rep && c < m0;
+        const int rr = on ? a.row_sel[c] : 0;
+        gcol[c] = (on && row) ? a.J[(b * a.ntasks * 6 + rr) * n + ic] : 0.0;
+        b0v[c] = on ? a.b0_scr[b * kM0Max + c] : 0.0;
+        acol[c] = gcol[c];
+    }
+    // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
+    // are rebuilt below)
+    {
+        // 64-bit addressing: the instances of a wave come from a work list (no uniform base)
+        const double *Mb = a.M + b * n * n + ic;
+        double A[NP];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+        __syncthreads();
+        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
+    }
+    WBQ_STAMP(9);
+    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0); warm start: the bound state of the last
+    // repair (any state is valid)
+    int st0 = 0;
+    if (row && warm) {
+        const int w = a.ws_state[b * NP + i];
+        st0 = (w < 0) ? -1 : (w > 0 ? 1 : 0);
+    }
+    double abm = 0.0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
+    abm = fmax(1.0, imax<NP>(fabs(abm)));
+    const double pintol = 1e-9 * abm;
+    const BvlsOut bv = bvls<NP, M0>(acol, b0v, m0, lo, hi, row, rep, st0, 50 * n + 100);
+    const double xv = bv.xv;
+    const int st = bv.st, it = bv.it;
+    if (bv.capped) out.status = 1;
     WBQ_STAMP(10);
     // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
     if (row) a.ws_state[b * NP + i] = (signed char)(st == 2 ? 0 : st);

@@ -187,14 +187,18 @@ int solve_contact(wbq_ctx *c, int integrate, double dt)
     a.stamps = c->stamps;
     a.integrate = integrate;
     a.dt = dt;
+    a.work = c->work;
+    a.wl = c->wl;
+    a.epoch = c->epoch;
     WBQ_HIP(hipSetDevice(c->device));
     const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
                        (c->solves++ % (unsigned long long)c->timing_every) == 0;
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
-    WBQ_HIP(wbq::launch_contact(a, c->stream));
-    if (timed) { // one kernel: the dominant kernel is the whole solve
+    WBQ_HIP(wbq::launch_contact(a, c->stream, timed ? c->ev[c->ev_used + 1] : nullptr));
+    if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
+    if (timed) {
         WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 2], c->stream));
-        c->ev_mid[c->ev_used / 3] = 2;
+        c->ev_mid[c->ev_used / 3] = 1;
         c->ev_used += 3;
     }
     return WBQ_SUCCESS;
@@ -344,6 +348,8 @@ int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
               hipMalloc(&c->dev_out, out_bytes) == hipSuccess &&
               hipHostMalloc((void **)&c->host_out, out_bytes, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->dev_x, B * c->nx * 8) == hipSuccess &&
+              hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
+              hipMalloc(&c->wl, B * sizeof(int)) == hipSuccess &&
               hipEventCreateWithFlags(&c->in_copied, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
     ok = hipMemcpy(c->tmax, tmx.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&

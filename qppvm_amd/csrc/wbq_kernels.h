@@ -92,6 +92,12 @@ struct ContactArgs {
     unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [B][kStamps] s_memtime
     int integrate;   // MPC rollout step: qdd = x[0:n], semi-implicit Euler on q, qd in place
     double dt;
+    // level-0 repair hand-off (as QppvmArgs): instances the main kernel finds level-0 infeasible at
+    // b_w are listed in wl (count work[epoch*2 + 1]) for the repair kernel, which clears the other
+    // parity's counters
+    int *work;       // [2][2]
+    int *wl;         // [B]
+    int epoch;
 };
 
 // Semi-implicit Euler of one joint of instance b in place (lane i owns joint i of its
@@ -107,7 +113,8 @@ __device__ __forceinline__ void rollout_step(const Args &a, long b, int i, bool 
     q[k] = q[k] + a.dt * v;
 }
 
-hipError_t launch_contact(const ContactArgs &a, hipStream_t stream);
+// mid (optional): recorded right after the main kernel, before the level-0 repair kernel
+hipError_t launch_contact(const ContactArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 
 // Lanes per instance used for a given n (32 for n <= 32, else 64).
 inline int lanes_per_instance(int n) { return n <= 32 ? 32 : 64; }

@@ -66,10 +66,49 @@ def qppvm_certificate(oracle, prob, inp, b, tau):
     return dict(primal=primal, level0=level0, stat=stat, sign=sign, indep=bool(indep))
 
 
-def contact_certificate(oracle, prob, inp, b, x):
-    """Scaled residuals of instance b's contact-form output x = [qdd; f]."""
+def contact_level0_certificate(oracle, prob, inp, b, x):
+    """Level-0 optimality of a contact-form output whose waist row is not at b_w (level 0 not
+    attainable): with tau = M qdd + h - J_c^T [f; 0] every row is a box in z = (tau_a, f) and the
+    waist value is y = A0 z - J_w M^-1 h (qppvm_amd/csrc/contact_kernel.hip:contact_level0), so z
+    must solve min 0.5 ||A0 z - (b_w + J_w M^-1 h)||^2 over the box: the gradient w = A0^T (b - A0 z)
+    vanishes on interior variables, w <= 0 at lower and w >= 0 at upper bounds. Returns the scaled
+    worst violation and y."""
+    a = oracle.contact_assemble(prob, inp, b)
+    n, nc = prob.n, prob.nc
+    M, h, Jw, Jc = inp["M"][b], inp["h"][b], inp["Jw"][b], inp["Jc"][b]
+    cm = int(inp["cmask"][b])
+    qdd, f = x[:n], x[n:]
+    tau = M @ qdd + h - sum(Jc[c, :3].T @ f[3 * c:3 * c + 3] for c in range(nc))
+    W = np.linalg.solve(M, Jw.T)
+    cols, z, lo, hi = [], [], [], []
+    for j in range(6, n):
+        cols.append(W[j]); z.append(tau[j])
+        lo.append(prob.tau_min[j] if prob.torque_rows else -np.inf)
+        hi.append(prob.tau_max[j] if prob.torque_rows else np.inf)
+    for k in range(3 * nc):
+        c, r = divmod(k, 3)
+        on = (cm >> c) & 1
+        cols.append(W.T @ Jc[c, r]); z.append(f[k])
+        lo.append(prob.f_lb[r] if on else 0.0); hi.append(prob.f_ub[r] if on else 0.0)
+    A0, z, lo, hi = np.array(cols).T, np.array(z), np.array(lo), np.array(hi)
+    bb = a["bw"] + W.T @ h
+    w = A0.T @ (bb - A0 @ z)
+    scale = np.abs(A0.T).sum(axis=1) * (np.abs(A0 @ z).max() + np.abs(bb).max()) + 1e-300
+    at_lo, at_hi = _active(z, lo, hi, 1e-8)
+    v = np.where(~(at_lo | at_hi), np.abs(w), 0.0)
+    v = np.maximum(v, np.where(at_lo & ~at_hi, np.maximum(w, 0.0), 0.0))
+    v = np.maximum(v, np.where(at_hi & ~at_lo, np.maximum(-w, 0.0), 0.0))
+    return float((v / scale).max()), Jw @ qdd
+
+
+def contact_certificate(oracle, prob, inp, b, x, waist=None):
+    """Scaled residuals of instance b's contact-form output x = [qdd; f]; waist (optional) replaces
+    the waist target b_w (level 1 after a level-0 repair keeps J_w qdd = y0*)."""
     a = oracle.contact_assemble(prob, inp, b)
     H, g, E, e, C, clo, chi = a["H"], a["g"], a["E"], a["e"], a["C"], a["clo"], a["chi"]
+    if waist is not None:
+        e = e.copy()
+        e[:6] = waist
     cx = C @ x
     scale = 1.0 + max(np.abs(e).max(), np.abs(np.concatenate([clo, chi])[np.isfinite(np.concatenate([clo, chi]))]).max(initial=0.0))
     primal = max(np.abs(E @ x - e).max(), max(0.0, (clo - cx).max(initial=0.0), (cx - chi).max(initial=0.0))) / scale
