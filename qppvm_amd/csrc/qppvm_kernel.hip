@@ -381,8 +381,14 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
         WBQ_STAMP(11);
         int status = ro.status, iters = 0;
         bool infeasible = false;
-        const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0, ro.lo, ro.hi, ro.u, status,
-                                            iters, infeasible);
+        // level 1 over a single feasible point needs no active set (rollouts do: they integrate
+        // u = M^-1 x, which the active set leaves in LDS)
+        const bool uniq = ro.unique && !a.integrate;
+        double x_i = ro.x;
+        if (__any(valid && !uniq))
+            x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
+                                   infeasible);
+        if (uniq) x_i = ro.x;
         WBQ_STAMP(12);
 #ifdef WBQ_STAMPS
         if (threadIdx.x == 0 && a.stamps) { // step counts of the diagnostic build

@@ -382,8 +382,10 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
 
 struct RepairOut {
     double lo, hi, u; // (possibly pinned) limits and the new u of this lane
+    double x;         // the BVLS point x* of this lane (level 0 in x-space)
     int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
     bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
+    bool unique;      // the level-1 feasible set is the single point x*: level 1 has nothing left
 };
 
 // Level-0 repair for the instances with rep set (every lane of the wave calls this; the
@@ -408,7 +410,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     const int n = a.n, m0 = a.m0;
     const int ic = i < n ? i : n - 1;
     const bool row = rep && i < n;
-    RepairOut out{lo, hi, 0.0, 0, 0, false};
+    RepairOut out{lo, hi, 0.0, 0.0, 0, 0, false, false};
     double gcol[M0], acol[M0], b0v[M0];
     const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
 #pragma unroll
@@ -433,12 +435,23 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
     }
     WBQ_STAMP(9);
-    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0); warm start: the bound state of the last
-    // repair (any state is valid)
+    // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0); warm start (any state is valid): the bound
+    // SET of the last repair, each variable on the side the level-0 gradient at that corner
+    // points to now. Under saturation a 1 kHz loop's torques can swap sides between ticks
+    // (a chattering plant): the last sides then cost one BVLS step per variable, this start
+    // a few (scripts/diag_plugin_tick.py, the config-0 stress plant: 42 -> 7 steps).
     int st0 = 0;
-    if (row && warm) {
-        const int w = a.ws_state[b * NP + i];
-        st0 = (w < 0) ? -1 : (w > 0 ? 1 : 0);
+    {
+        const int w = (row && warm) ? a.ws_state[b * NP + i] : 0;
+        const double xs = w < 0 ? lo : (w > 0 ? hi : (row ? fmin(fmax(0.0, lo), hi) : 0.0));
+        double rs0[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) rs0[c] = acol[c] * xs;
+        isum_vec<NP, M0>(rs0);
+        double g = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) g = fma(acol[c], b0v[c] - rs0[c], g);
+        if (w != 0) st0 = g > 0.0 ? 1 : -1;
     }
     double abm = 0.0;
 #pragma unroll
@@ -471,6 +484,25 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - ys[c], w);
         if (w > pintol) out.lo = hi;       // pinned at the upper bound
         else if (w < -pintol) out.hi = lo; // pinned at the lower bound
+    }
+    out.x = row ? xv : 0.0;
+    // Level 1 keeps A0 x = y* and the (pinned) box. When the columns of A0 over the variables
+    // left free are independent, x_F is fixed by A0_F x_F = y* - A0_P x_P: the feasible set is
+    // the single point x* and the level-1 objective cannot move it (the generic saturated case:
+    // the free columns span one facet of the zonotope A0 * box). The rank test is conservative
+    // (pivots above 1e-8 of the largest): a nearly dependent free set goes to the active set.
+    {
+        const bool fl = row && out.lo != out.hi;
+        double gf[NT];
+#pragma unroll
+        for (int p = 0; p < M0; ++p)
+#pragma unroll
+            for (int c = 0; c <= p; ++c) gf[tri(p, c)] = fl ? acol[p] * acol[c] : 0.0;
+        isum_vec<NP, NT>(gf);
+        const double kf = isum<NP>(fl ? 1.0 : 0.0);
+        PivChol<M0> pf;
+        pf.factor(gf, m0, 1e-8);
+        out.unique = rep && !bv.capped && (double)pf.k == kf;
     }
     double gg[NT], rr[M0];
 #pragma unroll

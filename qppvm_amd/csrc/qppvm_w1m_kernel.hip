@@ -437,6 +437,18 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
         __syncthreads(); // the previous instance's LDS is dead
         const RepairOut ro = level0_repair<64, M0>(a, 0, b, i, true, row ? a.tau_min[i] - h_i : -kInf,
                                                    row ? a.tau_max[i] - h_i : kInf, false);
+        if (ro.unique && !a.integrate) { // level 1 over a single feasible point: x = x* (wave-uniform)
+            int status = ro.status;
+            double tau_i = row ? ro.x + h_i : h_i;
+            if (imax<64>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+            if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+            if (row) a.tau[b * n + i] = tau_i;
+            if (i == 0) {
+                a.status[b] = status;
+                a.iters[b] = ro.it;
+            }
+            continue;
+        }
         // y* = G u at the least-distance point of G u = y* that the repair leaves in u
         double ys[M0];
 #pragma unroll

@@ -32,6 +32,7 @@ public:
     const Eigen::VectorXd &x() const { return _x; }
     const Eigen::VectorXd &qddot_value() const { return _qddot_value; }
     int last_status() const { return _status; }
+    int last_iters() const { return _iters; } // active-set + repair steps of the last solve
     int solver_errors() const { return _solver_errors; }
     // the per-tick solver inputs of the last control_loop (dumped by the dummy driver)
     const std::vector<double> &staged(int field) const { return _in[field]; }
@@ -49,6 +50,7 @@ private:
 
     double _start_time = 0.0;
     int _status = 0;
+    int _iters = 0;
     int _solver_errors = 0;
     int _cmask = 0xF;
 

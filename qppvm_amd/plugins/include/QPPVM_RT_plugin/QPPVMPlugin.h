@@ -30,6 +30,7 @@ public:
     // observability (the reference logs these to MatLogger: tau_qp, tau_desired)
     const Eigen::VectorXd &tau_desired() const { return _tau_d; }
     int last_status() const { return _status; }
+    int last_iters() const { return _iters; } // active-set + repair steps of the last solve
     int solver_errors() const { return _solver_errors; }
 
 private:
@@ -45,6 +46,7 @@ private:
     std::vector<std::string> _ee_links{"arm2_7", "arm1_7"};
     double _start_time = 0.0;
     int _status = 0;
+    int _iters = 0;
     int _solver_errors = 0;
 
     Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h;

@@ -138,6 +138,7 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
         wbq_get_contact_outputs(_ctx, _x.data()) != WBQ_SUCCESS)
         status = WBQ_STATUS_NUMERICAL;
     _status = status;
+    _iters = iters;
     if (status != WBQ_STATUS_OK) { // :189-193: "Unable to solve!!!", no command this tick
         ++_solver_errors;
         std::fprintf(stderr, "Unable to solve!!!\n");

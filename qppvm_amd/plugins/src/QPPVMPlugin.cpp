@@ -128,6 +128,7 @@ void QPPVMPlugin::QPPVMControl(double /*time*/) // :201-259
         for (int j = 0; j < n; ++j) _tau_d[j] = _h[j];
     }
     _status = status;
+    _iters = iters;
     if (status != WBQ_STATUS_OK) { // :246-249 -- tau_qp = 0, i.e. tau = h (already in tau)
         ++_solver_errors;
         std::fprintf(stderr, "SOLVER ERROR!\n");

@@ -18,6 +18,19 @@
 #include "abi_copy.h"
 #include "dummy_robot.h"
 
+#include <algorithm>
+
+// {"p50_us": .., "p99_us": ..} of the per-tick plugin times
+static std::string tick_percentiles(std::vector<double> us)
+{
+    if (us.empty()) return "\"p50_us\": 0, \"p99_us\": 0";
+    std::sort(us.begin(), us.end());
+    const double p50 = us[us.size() / 2], p99 = us[std::min(us.size() - 1, (size_t)(0.99 * us.size()))];
+    char buf[96];
+    std::snprintf(buf, sizeof(buf), "\"p50_us\": %.3f, \"p99_us\": %.3f", p50, p99);
+    return buf;
+}
+
 // ForceAcc in dummy mode: dump = header (n, nc, ticks), then per tick the 13 staged solver
 // input fields, the contact mask, tau, x and the status
 static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
@@ -42,6 +55,9 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
         std::fwrite(hdr, sizeof(int), 3, f);
     }
     double worst = 0.0, run_total = 0.0;
+    std::vector<double> tick_us;
+    tick_us.reserve((size_t)ticks);
+    int busy_ticks = 0; // ticks whose solve needed the active set or the level-0 repair
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = 0; k < ticks; ++k) {
         const auto a = std::chrono::steady_clock::now();
@@ -49,6 +65,8 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
         const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
         worst = us > worst ? us : worst;
         run_total += us;
+        tick_us.push_back(us);
+        busy_ticks += plugin.last_iters() > 0 ? 1 : 0;
         if (f && k < dump_ticks) {
             for (int fld = 0; fld < 13; ++fld)
                 std::fwrite(plugin.staged(fld).data(), sizeof(double), plugin.staged(fld).size(), f);
@@ -65,8 +83,9 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
     if (f) std::fclose(f);
     plugin.close();
     std::printf("{\"config\": 0, \"plugin\": \"ForceAccExample\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
-                "\"run_us\": %.3f, \"worst_us\": %.3f, \"solver_errors\": %d, \"sync_flags\": %d}\n", n, ticks,
-                total / ticks, run_total / ticks, worst, plugin.solver_errors(), handle->robot().last_sync());
+                "\"run_us\": %.3f, %s, \"worst_us\": %.3f, \"busy_ticks\": %d, \"solver_errors\": %d, \"sync_flags\": %d}\n",
+                n, ticks, total / ticks, run_total / ticks, tick_percentiles(tick_us).c_str(), worst, busy_ticks,
+                plugin.solver_errors(), handle->robot().last_sync());
     return 0;
 }
 
@@ -74,11 +93,12 @@ int main(int argc, char **argv)
 {
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
-    bool forceacc = false;
+    bool forceacc = false, stress = false;
     for (int k = 1; k < argc; ++k) {
         if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
         else if (!std::strcmp(argv[k], "--n") && k + 1 < argc) n = std::atoi(argv[++k]);
         else if (!std::strcmp(argv[k], "--plugin") && k + 1 < argc) forceacc = !std::strcmp(argv[++k], "forceacc");
+        else if (!std::strcmp(argv[k], "--stress")) stress = true;
         else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
             dump = argv[++k];
             dump_ticks = std::atoi(argv[++k]);
@@ -88,6 +108,7 @@ int main(int argc, char **argv)
     if (n <= 0) n = 39;
     dummy::Params prm;
     prm.n = n;
+    if (stress) prm.jscale = 0.5;
     auto handle = std::make_shared<dummy::Handle>(prm);
     demo::QPPVMPlugin plugin;
     if (!plugin.init_control_plugin(handle)) {
@@ -117,6 +138,9 @@ int main(int argc, char **argv)
         handle->robot().set_state(q, qd);
     }
     double worst = 0.0, run_total = 0.0;
+    std::vector<double> tick_us;
+    tick_us.reserve((size_t)ticks);
+    int busy_ticks = 0; // ticks whose solve needed the active set or the level-0 repair
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = 0; k < ticks; ++k) {
         const double time = (k + 1) * dt;
@@ -125,6 +149,8 @@ int main(int argc, char **argv)
         const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
         worst = us > worst ? us : worst;
         run_total += us;
+        tick_us.push_back(us);
+        busy_ticks += plugin.last_iters() > 0 ? 1 : 0;
         if (f && k < dump_ticks) {
             // the solver inputs of this tick, recomputed from the (unchanged) model state
             auto &m = handle->model();
@@ -161,8 +187,10 @@ int main(int argc, char **argv)
     plugin.close();
     // us_per_tick: the whole loop (plugin tick + dummy model + physics); run_us: the plugin
     // tick alone (model queries, one wbq solve, torque write-back)
-    std::printf("{\"config\": 0, \"plugin\": \"QPPVMPlugin\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, \"run_us\": %.3f, "
-                "\"worst_us\": %.3f, \"solver_errors\": %d}\n", n, ticks, total / ticks, run_total / ticks, worst,
+    std::printf("{\"config\": 0, \"plugin\": \"QPPVMPlugin\", \"plant\": \"%s\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
+                "\"run_us\": %.3f, %s, \"worst_us\": %.3f, \"busy_ticks\": %d, \"solver_errors\": %d}\n",
+                stress ? "stress (jscale 0.5, saturating)" : "nominal (jscale 0.2)", n, ticks, total / ticks,
+                run_total / ticks, tick_percentiles(tick_us).c_str(), worst, busy_ticks,
                 plugin.solver_errors());
     return 0;
 }

@@ -21,6 +21,13 @@ struct Params {
     // quadruped (pelvis + 4 feet) for the ForceAcc plugin
     std::vector<std::string> links{"arm2_7", "arm1_7"};
     bool floating_base = false; // first 6 coordinates = floating base; gravity on its z row
+    // Jacobian entry scale (lever arms, m). 0.2 keeps the operational-space inverse inertia
+    // J M^-1 J^T ~ O(1) as on a real arm, so the reference gains (Dc = 70) are stable under the
+    // 1 kHz explicit step (Dc * lambda_max(J M^-1 J^T) * dt < 2) and the 150 Nm limits bind only
+    // now and then. 0.5 (--stress, the round-1 plant) gives lambda_max ~ 1e2: the closed loop
+    // chatters, every joint saturates and the torques swap sides every tick -- a level-0
+    // repair on every tick, kept as the worst case of the repair path.
+    double jscale = 0.2;
 };
 
 inline Params quadruped(int n = 30)
@@ -30,6 +37,7 @@ inline Params quadruped(int n = 30)
     p.seed = 11;
     p.links = {"pelvis", "foot_fl", "foot_fr", "foot_hr", "foot_hl"};
     p.floating_base = true;
+    p.jscale = 0.5;
     return p;
 }
 
@@ -61,7 +69,7 @@ public:
         J0_.assign(nl, std::vector<double>((size_t)6 * n_, 0.0));
         p0_.assign(nl, std::vector<double>(3, 0.0));
         for (int t = 0; t < nl; ++t) {
-            for (auto &v : J0_[t]) v = 0.5 * N(g);
+            for (auto &v : J0_[t]) v = p.jscale * N(g);
             if (fb_ && t == 0) { // the base link moves with the floating base only
                 for (auto &v : J0_[t]) v = 0.0;
                 for (int r = 0; r < 6; ++r) J0_[t][r * n_ + r] = 1.0;

@@ -25,8 +25,9 @@ def main():
     lib = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "qppvm_amd", "libwbq_diag.so")
     ticks = int(os.environ.get("DIAG_TICKS", "40"))
     dump = "/tmp/diag_tick_dump.bin"
+    stress = ["--stress"] if os.environ.get("DIAG_STRESS") == "1" else []
     subprocess.run([os.path.join(ROOT, "qppvm_amd", "qppvm_dummy_driver"), "--ticks", str(ticks), "--dump", dump,
-                    str(ticks)], check=True, capture_output=True)
+                    str(ticks)] + stress, check=True, capture_output=True)
     n, d = read_dump(dump)
     prob = QPPVMProblem(n=n, tau_max=150.0)
     wbq._lib = None

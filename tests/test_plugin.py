@@ -40,12 +40,16 @@ def read_dump(path):
     return int(n), out
 
 
-def test_dummy_driver_matches_oracle(tmp_path, oracle_lib):
+@pytest.mark.parametrize("plant", ["nominal", "stress"])
+def test_dummy_driver_matches_oracle(tmp_path, oracle_lib, plant):
+    """QPPVMPlugin in dummy mode; every dumped tick re-solved by the oracle. The stress plant
+    saturates every joint on every tick with the torques swapping sides (the level-0 repair on
+    every tick: warm-started BVLS, pins, the single-point level 1)."""
     from qppvm_amd import build
     driver = build.build_plugins()[1]
     dump = str(tmp_path / "dump.bin")
-    r = subprocess.run([driver, "--ticks", "300", "--dump", dump, "40"], capture_output=True, text=True,
-                       timeout=240)
+    r = subprocess.run([driver, "--ticks", "300", "--dump", dump, "40"] + (["--stress"] if plant == "stress" else []),
+                       capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     n, d = read_dump(dump)
     prob = QPPVMProblem(n=n, tau_max=150.0)
