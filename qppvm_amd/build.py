@@ -63,7 +63,7 @@ DRIVER_RM = os.path.join(HERE, "qppvm_dummy_driver_rowmajor")
 
 def _plugin_sources():
     out = []
-    for d in ("src", "include/QPPVM_RT_plugin", "include/ForceAccPlugin", "compat/XCM"):
+    for d in ("src", "include/QPPVM_RT_plugin", "include/ForceAccPlugin", "compat/XCM", "compat/XBotInterface"):
         base = os.path.join(PLUGIN_DIR, d)
         out += [os.path.join(base, f) for f in os.listdir(base)]
     return out

@@ -17,8 +17,17 @@ constexpr double kInf = 1.0e300;
         __builtin_amdgcn_sched_barrier(0);                                              \
         if (threadIdx.x == 0 && a.stamps) a.stamps[blockIdx.x * kStamps + (k)] = t_;    \
     } while (0)
+// the constant 100 MHz clock, synchronised across XCDs (s_memtime is per-XCD)
+#define WBQ_RTSTAMP(k)                                                                  \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (threadIdx.x == 0 && a.stamps) a.stamps[blockIdx.x * kStamps + (k)] = t_;    \
+    } while (0)
 #else
 #define WBQ_STAMP(k) do {} while (0)
+#define WBQ_RTSTAMP(k) do {} while (0)
 #endif
 
 // Workgroup barrier that orders LDS only. __syncthreads() is a workgroup fence on every

@@ -53,7 +53,7 @@ struct QppvmArgs {
     double dt;
 };
 
-constexpr int kStamps = 16; // fast 0-3,5; active-set 4,6,7; repair 8-12
+constexpr int kStamps = 20; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12
 
 // Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
 // device and kernel; thread-safe: contexts on several devices or threads share it).

@@ -9,6 +9,7 @@
 // plugin, allocated in init_control_plugin.
 #pragma once
 
+#include <XBotInterface/Logger.hpp>
 #include <XCM/XBotControlPlugin.h>
 
 #include <cstdint>
@@ -37,6 +38,8 @@ public:
     // the per-tick solver inputs of the last control_loop (dumped by the dummy driver)
     const std::vector<double> &staged(int field) const { return _in[field]; }
     int contact_mask() const { return _cmask; }
+    // the reference hard-codes "/tmp/opensot_force_acc_example" (ForceAcc.cpp:34)
+    void set_log_prefix(const std::string &prefix) { _log_prefix = prefix; }
 
 protected:
     void control_loop(double time, double period) override;
@@ -63,6 +66,8 @@ private:
     // staged wbq_contact_inputs fields (M, h, q, qd, qref, Jw, jdqd_w, pose_w, pose_w_ref,
     // Jc, jdqd_c, pose_c, pose_c_ref), one instance
     std::vector<double> _in[13];
+    std::string _log_prefix = "/tmp/opensot_force_acc_example";
+    XBot::MatLogger::Ptr _logger;
 };
 
 }  // namespace XBotPlugin

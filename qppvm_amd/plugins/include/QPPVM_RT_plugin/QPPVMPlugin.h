@@ -7,6 +7,7 @@
 // (include/wbq.h); one wbq context per plugin, allocated in init_control_plugin.
 #pragma once
 
+#include <XBotInterface/Logger.hpp>
 #include <XCM/XBotControlPlugin.h>
 
 #include <cstdint>
@@ -32,6 +33,11 @@ public:
     int last_status() const { return _status; }
     int last_iters() const { return _iters; } // active-set + repair steps of the last solve
     int solver_errors() const { return _solver_errors; }
+    // the reference hard-codes both (QPPVMPlugin.cpp:44 "/tmp/qppvm_log", :46 _set_ref = false);
+    // the dummy driver sets them before init_control_plugin / on_start
+    void set_log_prefix(const std::string &prefix) { _log_prefix = prefix; }
+    void set_reference_trajectory(bool on) { _set_ref = on; }
+    const Eigen::Affine3d &ee_reference(int t) const { return _ref[t]; }
 
 private:
     void sense();
@@ -52,6 +58,11 @@ private:
     Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h;
     Eigen::VectorXd _tau_max_const, _tau_min_const;
     Eigen::Affine3d _ref[2];
+    // _set_ref: left end-effector reference on a circle in the y-z plane (:217-223)
+    bool _set_ref = false;
+    Eigen::Affine3d _start_pose;
+    std::string _log_prefix = "/tmp/qppvm_log";
+    XBot::MatLogger::Ptr _matlogger;
     // per-tick input staging (instance-major, row-major: the wbq layout)
     std::vector<double> _M, _J, _pose, _pose_ref;
 };

@@ -20,6 +20,8 @@ ForceAccExample::~ForceAccExample()
 bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
 {
     _robot = handle->getRobotInterface();
+    _logger = XBot::MatLogger::getLogger(_log_prefix); // :34
+    _logger->reserve(10000);                           // _model->initLog(_logger, 10000) (:50)
     _robot->getStiffness(_k); // :36-39: impedance / 16, damping / 4
     _robot->getDamping(_d);
     for (size_t j = 0; j < _k.size(); ++j) {
@@ -146,6 +148,19 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     }
     for (int j = 0; j < n; ++j) _qddot_value[j] = _x[j]; // :196
     _tau = tau;                                          // ID(q, qd, qdd) - tau_c (:206-218)
+    // logs (:200, :233-236): wrench w_c = [f_c; 0] per contact, tau_c = sum_c J_c^T w_c
+    Eigen::VectorXd tau_c(n, 0.0), w(6, 0.0);
+    for (size_t c = 0; c < nc; ++c) {
+        for (int k = 0; k < 3; ++k) w[k] = _x[n + 3 * c + k];
+        const double *Jc = _in[9].data() + c * 6 * n; // row-major 6 x n
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < n; ++j) tau_c[j] += Jc[k * n + j] * w[k];
+        _logger->add(_contact_links[c] + "_wrench", w);
+    }
+    _logger->add("tau", _tau);
+    _logger->add("tau_c", tau_c);
+    _logger->add("qddot_value", _qddot_value);
+    _logger->add("x", _x);
     _model->setJointEffort(_tau);                        // :219
     _robot->setStiffness(_k);                            // :239-241 (re-sent every tick)
     _robot->setDamping(_d);
@@ -165,6 +180,7 @@ void ForceAccExample::sync_model() // :256-282; floating-base state comes with t
 
 bool ForceAccExample::close() // ForceAcc.h:43
 {
+    if (_logger) _logger->flush();
     if (_ctx) {
         wbq_destroy(_ctx);
         _ctx = nullptr;

@@ -2,6 +2,7 @@
 // (src/QPPVMPlugin.cpp), with the OpenSoT/qpOASES solve replaced by one wbq_solve.
 #include <QPPVM_RT_plugin/QPPVMPlugin.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 
@@ -21,8 +22,10 @@ QPPVMPlugin::~QPPVMPlugin()
 bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle)
 {
     _robot = handle->getRobotInterface();
+    _matlogger = XBot::MatLogger::getLogger(_log_prefix); // :44
     _model = handle->getModel(); // reference: hard-coded CENTAURO yaml (:50-51)
     const int n = _model->getJointNum();
+    _matlogger->reserve(30000); // _model->initLog(_matlogger, 30000) (:54)
 
     _model->getEffortLimits(_tau_max_const); // :56-58
     _tau_min_const.setZero(n);
@@ -91,11 +94,17 @@ void QPPVMPlugin::on_start(double time) // :261-305
     // references = current poses and current q (:271-279)
     for (int t = 0; t < 2; ++t) _model->getPose(_ee_links[t], _ref[t]);
     _q_ref = _q;
+    _model->getPose(_ee_links[1], _start_pose); // left end effector (:284)
 }
 
-void QPPVMPlugin::QPPVMControl(double /*time*/) // :201-259
+void QPPVMPlugin::QPPVMControl(double time) // :201-259
 {
     const int n = _model->getJointNum();
+    if (_set_ref) { // :217-223 -- y += 0.15 sin(t - t0), z += 0.15 (1 - cos(t - t0)) on the left task
+        _ref[1] = _start_pose;
+        _ref[1].m[7] = _start_pose.m[7] + 0.15 * std::sin(time - _start_time);
+        _ref[1].m[11] = _start_pose.m[11] + 0.15 * (1.0 - std::cos(time - _start_time));
+    }
     Eigen::MatrixXd M, J;
     // element-wise into the ABI's row-major layout (include/wbq.h): Eigen's MatrixXd is
     // column-major, so its data() is never copied as is
@@ -133,6 +142,10 @@ void QPPVMPlugin::QPPVMControl(double /*time*/) // :201-259
         ++_solver_errors;
         std::fprintf(stderr, "SOLVER ERROR!\n");
     }
+    Eigen::VectorXd tau_qp(n, 0.0);
+    for (int j = 0; j < n; ++j) tau_qp[j] = _tau_d[j] - _h[j];
+    _matlogger->add("tau_qp", tau_qp);       // :254
+    _matlogger->add("tau_desired", _tau_d); // :258
 }
 
 void QPPVMPlugin::control_loop(double time, double /*period*/) // :308-329
@@ -142,6 +155,7 @@ void QPPVMPlugin::control_loop(double time, double /*period*/) // :308-329
     QPPVMControl(time);
     _model->setJointEffort(_tau_d);
     _robot->setReferenceFrom(*_model, XBot::Sync::Effort);
+    _matlogger->add("time_matlogger", time); // :322
     _robot->move();
 }
 
@@ -154,6 +168,7 @@ void QPPVMPlugin::sense() // :331-336
 
 bool QPPVMPlugin::close() // :339-342 (the reference is missing its return)
 {
+    if (_matlogger) _matlogger->flush();
     if (_ctx) {
         wbq_destroy(_ctx);
         _ctx = nullptr;

@@ -33,10 +33,11 @@ static std::string tick_percentiles(std::vector<double> us)
 
 // ForceAcc in dummy mode: dump = header (n, nc, ticks), then per tick the 13 staged solver
 // input fields, the contact mask, tau, x and the status
-static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks)
+static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, const char *log_prefix)
 {
     auto handle = std::make_shared<dummy::Handle>(dummy::quadruped(n));
     XBotPlugin::ForceAccExample plugin;
+    if (log_prefix) plugin.set_log_prefix(log_prefix);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;
@@ -93,24 +94,29 @@ int main(int argc, char **argv)
 {
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
-    bool forceacc = false, stress = false;
+    bool forceacc = false, stress = false, set_ref = false;
+    const char *log_prefix = nullptr;
     for (int k = 1; k < argc; ++k) {
         if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
         else if (!std::strcmp(argv[k], "--n") && k + 1 < argc) n = std::atoi(argv[++k]);
         else if (!std::strcmp(argv[k], "--plugin") && k + 1 < argc) forceacc = !std::strcmp(argv[++k], "forceacc");
         else if (!std::strcmp(argv[k], "--stress")) stress = true;
+        else if (!std::strcmp(argv[k], "--set-ref")) set_ref = true; // QPPVMPlugin.cpp:217-223
+        else if (!std::strcmp(argv[k], "--log") && k + 1 < argc) log_prefix = argv[++k];
         else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
             dump = argv[++k];
             dump_ticks = std::atoi(argv[++k]);
         }
     }
-    if (forceacc) return run_forceacc(ticks, n > 0 ? n : 30, dump, dump_ticks);
+    if (forceacc) return run_forceacc(ticks, n > 0 ? n : 30, dump, dump_ticks, log_prefix);
     if (n <= 0) n = 39;
     dummy::Params prm;
     prm.n = n;
     if (stress) prm.jscale = 0.5;
     auto handle = std::make_shared<dummy::Handle>(prm);
     demo::QPPVMPlugin plugin;
+    if (log_prefix) plugin.set_log_prefix(log_prefix);
+    plugin.set_reference_trajectory(set_ref);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;

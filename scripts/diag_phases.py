@@ -30,7 +30,7 @@ def run(libpath, prob, inp, reps=20, stamps=False):
     if stamps:
         B = inp["h"].shape[0]
         nb = B if (prob.n > 32 or os.environ.get("WBQ_MFMA_MAX_BATCH", "1") != "0") else (B + 1) // 2
-        K = 16
+        K = 20
         buf = (ctypes.c_ulonglong * (K * nb))()
         s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         assert s.lib.wbq_diag_stamps(s.ctx, buf, nb) == 0
@@ -38,7 +38,18 @@ def run(libpath, prob, inp, reps=20, stamps=False):
         st = full[:, [0, 1, 2, 3, 5]]
         d = np.diff(st, axis=1)
         out["fast_kernel_phase_cycles_mean"] = {p: float(d[:, k].mean()) for k, p in enumerate(PHASES)}
+        out["fast_kernel_phase_cycles_mean"]["(stage: loads issued + forces)"] = float((full[:, 15] - full[:, 0]).mean())
+        out["fast_kernel_phase_cycles_mean"]["(stage: wait for M + Y)"] = float((full[:, 1] - full[:, 15]).mean())
         out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
+        rt = full[:, 16:18]  # s_memrealtime (100 MHz, global): start / end offsets in us
+        t0 = rt[:, 0].min()
+        out["fast_block_start_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 0] - t0, q)) / 100 for q in (10, 50, 90, 100)]
+        out["fast_block_end_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 1] - t0, q)) / 100 for q in (10, 50, 90, 100)]
+        out["fast_block_dur_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 1] - rt[:, 0], q)) / 100 for q in (10, 50, 90, 100)]
+        # by XCD (round-robin block dispatch: XCD = block id % 8)
+        xcd = np.arange(nb) % 8
+        out["fast_block_dur_us_mean_by_xcd"] = [float((rt[xcd == x, 1] - rt[xcd == x, 0]).mean()) / 100 for x in range(8)]
+        out["fast_block_cycles_mean_by_xcd"] = [float((st[xcd == x, -1] - st[xcd == x, 0]).mean()) for x in range(8)]
         _, status, iters = s.outputs()
         it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if nb < B else iters[:nb]
         act = it_blk > 0
@@ -75,8 +86,9 @@ def main():
     for B in (256, 1024, 4096, 16384, 65536):
         inp = replicate({k: v[:1] for k, v in base.items()}, B)
         res[f"cfg1_B{B}"] = run(wbq.LIB_PATH, p1, inp)
-    inp = replicate({k: v[:1] for k, v in base.items()}, 4096)
-    res["cfg1_B4096_stamps"] = run(diag, p1, inp, stamps=True)
+    for B in (256, 4096):
+        inp = replicate({k: v[:1] for k, v in base.items()}, B)
+        res[f"cfg1_B{B}_stamps"] = run(diag, p1, inp, stamps=True)
     free = wbq.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=4096)
     sub = {k: v[:4096] for k, v in base.items()}
     tau_free, _, _ = free.solve_batch(sub)
