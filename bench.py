@@ -64,8 +64,9 @@ def shard_plan(config, B, world, global_batch):
     return ShardPlan(global_batch if config == 3 else B * world, world)
 
 
-def build_workload(form, config, n, B, world, rank, device, weight=0, global_batch=65536):
-    """(problem, inputs, solver class) for this rank's shard (weight: joint task W1 = I / M)."""
+def build_workload(form, config, n, B, world, rank, device, weight=0, global_batch=65536, plant=False):
+    """(problem, inputs, solver class) for this rank's shard (weight: joint task W1 = I / M;
+    plant: the physically scaled synthetic states of config 4, qppvm_amd/synth.py)."""
     from qppvm_amd.problem import ContactProblem, QPPVMProblem
     from qppvm_amd.synth import contact_instances, qppvm_instances, replicate
     from qppvm_amd.wbq import ContactSolver, QPPVMSolver
@@ -77,11 +78,11 @@ def build_workload(form, config, n, B, world, rank, device, weight=0, global_bat
         if config == 1:
             prob = QPPVMProblem(n=n, tau_max=1e6, joint_weight=weight)  # bounds inactive
             return prob, replicate(qppvm_instances(prob, 1, seed=0), B), QPPVMSolver
-        inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank))
+        inp = qppvm_instances(QPPVMProblem(n=n), plan.count(rank), seed=1, offset=plan.start(rank), plant=plant)
         # ~20 % of the torque limits binding: tau_max = 80th percentile of |tau| of the first
         # B instances solved with the limits far away (same sample on every rank)
         # (the calibration sample is the first 4096 instances of the global batch, on every rank)
-        calib = qppvm_instances(QPPVMProblem(n=n), min(4096, plan.total), seed=1, offset=0)
+        calib = qppvm_instances(QPPVMProblem(n=n), min(4096, plan.total), seed=1, offset=0, plant=plant)
         free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9, joint_weight=weight), max_batch=calib["h"].shape[0],
                            device=device)
         tau_free, _, _ = free.solve_batch(calib)
@@ -114,12 +115,28 @@ def churn_pool(form, prob, n, B, world, rank):
                              masks=[0b0011, 0b0111, 0b1111])
 
 
+def euler_stability(prob, inp, dt, sample=256):
+    """dt * Dc * lambda_max(G_t M^-1 G_t^T) per instance (max over the tasks; G_t = the task's
+    selected Jacobian rows): the explicit-Euler factor of the task damping. Above 2 the
+    closed loop of an MPC rollout with frozen J, M is unstable at this dt."""
+    out = []
+    for b in range(min(sample, inp["h"].shape[0])):
+        Minv = np.linalg.inv(inp["M"][b])
+        worst = 0.0
+        for t in range(prob.ntasks):
+            rows = [r for r in range(6) if (prob.row_mask[t] >> r) & 1]
+            G = inp["J"][b, t][rows]
+            worst = max(worst, float(np.linalg.eigvalsh(G @ Minv @ G.T).max()) * float(prob.Dc[t].max()))
+        out.append(dt * worst)
+    return {"median": float(np.median(out)), "max": float(np.max(out)), "instances": len(out)}
+
+
 def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False,
-        weight=0, global_batch=65536):
+        weight=0, global_batch=65536, plant=False):
     """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
     import torch
     plan = shard_plan(config, B, world, global_batch)
-    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device, weight, global_batch)
+    prob, inp, Solver = build_workload(form, config, n, B, world, rank, device, weight, global_batch, plant)
     B = plan.count(rank)
     solver = Solver(prob, max_batch=max(B, 1), device=device)
     solver.set_inputs(inp)
@@ -213,6 +230,19 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
     solve_ms, kern_ms, launches = solver.get_timing_detail()
     ag_ms = float(np.mean([a.elapsed_time(b) for a, b in ag_events])) if ag_events else 0.0
     tau, status, iters = solver.outputs()
+    mpc = None
+    if config == 4 and form == "qppvm":
+        # repair share: one more rollout from the measured state, one step per call, reading the
+        # warm-start hints (1 = that step's level 0 was infeasible: the BVLS repair ran)
+        solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
+        shares = []
+        for _ in range(HORIZON):
+            solver.rollout(1, MPC_DT)
+            shares.append(float(solver.warm_hints().mean()))
+        mpc = {"repair_share_per_step": float(np.mean(shares)), "repair_share_last_step": shares[-1],
+               "euler_dt_Dc_lambda_max": euler_stability(prob, inp, MPC_DT),
+               "inputs": "plant-scaled (lambda(M) in [0.5, 5], J ~ N(0, 0.2^2))" if plant else
+                         "SURVEY 8d distribution (lambda(M) in [1e-2, 1e1], J ~ N(0, 0.5^2))"}
     if gather_buf is not None:  # the gathered tau holds this rank's shard where the plan puts it
         g = gather_buf[rank * plan.max_count: rank * plan.max_count + B].cpu().numpy()
         assert np.array_equal(g, tau), "all-gathered tau differs from the rank's own solve"
@@ -226,7 +256,7 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
     qps = HORIZON if config == 4 else 1  # an MPC step counts its N sequential QPs
     return dict(prob=prob, inp=inp, dt=dt, t_enq=t_enq, kavg_ms=kavg_ms, savg_ms=savg_ms, status=status, iters=iters,
                 bytes_per_instance=per_inst, total=plan.total * steps * qps, B_local=B, allgather_ms=ag_ms,
-                allgather_bytes=8 * n * plan.max_count * world)
+                allgather_bytes=8 * n * plan.max_count * world, mpc=mpc)
 
 
 def dominant_kernel(form, weight):
@@ -248,7 +278,7 @@ def pmc_traffic(args, form):
                    sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-pmc", "--no-variant",
                    "--steps", "20", "--warmup", "2", "--form", form, "--config", str(args.config),
                    "--batch", str(args.batch), "--global-batch", str(args.global_batch), "--n", str(args.n),
-                   "--weight", args.weight]
+                   "--weight", args.weight, "--mpc-inputs", args.mpc_inputs]
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
@@ -287,6 +317,28 @@ def cpu_baseline(form, prob, inp, budget_s):
             "contact-form assembly + dense dual active set with LU-solved KKT")
     return {"value": done / dt, "unit": "QP-solves/s", "cores": 1, "kind": "port",
             "sample": f"{done} instances of the bench batch in {dt:.1f} s, oracle ({what}), 1 thread"}
+
+
+def cpu_baseline_mpc(prob, inp, budget_s, rollouts=32):
+    """Config 4 on the CPU: the oracle solves each step of a bounded sample of rollouts, numpy
+    integrates (q_dd = M^-1 (tau - h), semi-implicit Euler), HORIZON steps per rollout."""
+    import oracle
+    oracle.build()
+    done, t0, B = 0, time.perf_counter(), inp["h"].shape[0]
+    while time.perf_counter() - t0 < budget_s:
+        lo = (done // HORIZON) % B
+        cur = {k: v[lo:lo + rollouts].copy() for k, v in inp.items()}
+        for _ in range(HORIZON):
+            tau, st, _ = oracle.qppvm_batch(prob, cur)
+            qdd = np.linalg.solve(cur["M"], (tau - cur["h"])[..., None])[..., 0]
+            qdd[st != 0] = 0.0
+            cur["qd"] = cur["qd"] + MPC_DT * qdd
+            cur["q"] = cur["q"] + MPC_DT * cur["qd"]
+        done += cur["h"].shape[0] * HORIZON
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "QP-solves/s", "cores": 1, "kind": "port",
+            "sample": f"{done // HORIZON} rollouts x {HORIZON} steps of the bench batch in {dt:.1f} s, oracle per "
+                      "step + numpy Euler, 1 thread"}
 
 
 def cpu_baseline_threads(form, prob, inp, budget_s):
@@ -360,6 +412,9 @@ def main():
                          "3: a fixed global batch of random states sharded over the GPUs + all-gather of tau; "
                          "4: MPC, each step = HORIZON sequential solves per rollout (wbq_rollout)")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step (config 3: always)")
+    ap.add_argument("--mpc-inputs", choices=("plant", "survey"), default="plant",
+                    help="config 4 states: plant-scaled (stable explicit Euler at the reference gains, default) "
+                         "or the SURVEY 8d distribution (its rollouts diverge into level-0 repairs)")
     ap.add_argument("--weight", choices=("I", "M"), default="I", help="QPPVM joint-task weight W1 (SURVEY 8a a6)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -397,8 +452,9 @@ def main():
     n, B = args.n, args.batch
     weight = 1 if args.weight == "M" else 0
     kern = dominant_kernel(args.form, weight)
+    plant = args.config == 4 and args.mpc_inputs == "plant"
     m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, allgather, dist,
-            args.host_io, weight, args.global_batch)
+            args.host_io, weight, args.global_batch, plant)
     value = m["total"] / m["dt"]
     bpl = m["bytes_per_instance"] * m["B_local"]
     achieved = bpl / (m["kavg_ms"] * 1e-3) / 1e9
@@ -449,6 +505,8 @@ def main():
         "max_active_set_steps": int(it.max()) if it.size else 0,
         "host_enqueue_us_per_step": m["t_enq"] * 1e6 / args.steps,
     }
+    if m["mpc"] is not None:
+        line["mpc"] = m["mpc"]
     if allgather:
         line["allgather"] = {"avg_ms": m["allgather_ms"], "bytes": m["allgather_bytes"],
                              "note": "torch.cuda events around all_gather_into_tensor (RCCL) on every "
@@ -464,8 +522,11 @@ def main():
                                    "status_ok_frac": float(np.mean(v["status"] == 0)),
                                    "mean_active_set_steps": float(np.mean(v["iters"]))}
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(args.form, m["prob"], m["inp"], args.cpu_seconds)
-        line["cpu_baseline_threads"] = cpu_baseline_threads(args.form, m["prob"], m["inp"], args.cpu_seconds / 2)
+        if args.config == 4 and args.form == "qppvm":
+            line["cpu_baseline"] = cpu_baseline_mpc(m["prob"], m["inp"], args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = cpu_baseline(args.form, m["prob"], m["inp"], args.cpu_seconds)
+            line["cpu_baseline_threads"] = cpu_baseline_threads(args.form, m["prob"], m["inp"], args.cpu_seconds / 2)
         line["cpu_host"] = host_cpu()
     if rank == 0:
         print(json.dumps(line), flush=True)

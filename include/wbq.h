@@ -178,6 +178,10 @@ int wbq_get_device_outputs(wbq_ctx *ctx, const double **tau, const int32_t **sta
  * mask has one entry per instance of the last wbq_set_inputs batch); NULL = every instance up
  * to max_batch. Stream-ordered with the solves. */
 int wbq_reset_warmstart(wbq_ctx *ctx, const uint8_t *mask);
+/* Read the per-instance warm-start hints of the current batch (1 = the last solve of that
+ * instance went through the level-0 repair with level 0 infeasible at b0; all 0 in a form
+ * without hints): diagnostics, e.g. the repair share of MPC rollout steps. Synchronous. */
+int wbq_get_warmstart_hints(wbq_ctx *ctx, uint8_t *hints);
 /* Kernel timing with HIP events on the launch stream: enable = N > 0 times every N-th solve
  * (events are stream packets: sampling keeps them from pacing the stream), 0 disables; then
  * read the summed device time (ms) and the number of timed solves since the last read. */

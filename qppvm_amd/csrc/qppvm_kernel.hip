@@ -348,9 +348,60 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     }
 }
 
-// Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by the
-// active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. Rare path:
-// kept out of the other kernels so that its registers do not weigh on them.
+// Inlined into the fast kernel (n <= 32): A/B on MI355X (profiles/r02_v5_ab_*), config 1
+// 96.9 -> 107.5 M QP/s (the follow-up launch is gone); as a real call (noinline) the call
+// frame slows the whole fast kernel (89.0 M QP/s).
+#ifndef WBQ_REPAIR_INLINE
+#define WBQ_REPAIR_INLINE __forceinline__
+#endif
+// Level-0 repair of one instance (the lanes with rep set; every lane of the wave calls it):
+// y* by BVLS, the pins, and a fresh dual active set (or, when the pinned level-0 point is the
+// only feasible one, that point) -> tau, status, iters, warm-start hint. S is the instance's
+// active-set LDS. Shared by the repair kernel (n > 32) and the fast kernel for n <= 32 (there a
+// solve is one launch).
+template <int NP, int M0>
+__device__ WBQ_REPAIR_INLINE void repair_instance(const QppvmArgs &a, double *S, long b, int i, bool rep)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int n = a.n;
+    const bool row = rep && i < n;
+    const double h_i = row ? a.h[b * n + i] : 0.0;
+    const bool warm = rep && a.ws_hint[b] != 0;
+    const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, rep, row ? a.tau_min[i] - h_i : -kInf,
+                                               row ? a.tau_max[i] - h_i : kInf, warm);
+    WBQ_STAMP(11);
+    int status = ro.status, iters = 0;
+    bool infeasible = false;
+    // level 1 over a single feasible point needs no active set (rollouts do: they integrate
+    // u = M^-1 x, which the active set leaves in LDS)
+    const bool uniq = ro.unique && !a.integrate;
+    double x_i = ro.x;
+    if (__any(rep && !uniq))
+        x_i = gi_solve<NP, M0>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
+                               infeasible);
+    if (uniq) x_i = ro.x;
+    WBQ_STAMP(12);
+#ifdef WBQ_STAMPS
+    if (threadIdx.x == 0 && a.stamps) { // step counts of the diagnostic build
+        a.stamps[blockIdx.x * kStamps + 13] = (unsigned long long)ro.it;
+        a.stamps[blockIdx.x * kStamps + 14] = (unsigned long long)iters;
+    }
+#endif
+    if (infeasible && status == 0) status = 2;
+    double tau_i = x_i + h_i;
+    if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+    if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
+    if (row) a.tau[b * n + i] = tau_i;
+    rollout_step(a, b, i, row, S[ActiveLayout<NP>(a.ntasks, a.m0).U + i], status == 0);
+    if (rep && (i & (NP - 1)) == 0) {
+        a.status[b] = status;
+        a.iters[b] = iters + ro.it;
+        a.ws_hint[b] = ro.l0inf ? 1 : 0;
+    }
+}
+
+// Level-0 repair kernel (n > 32): instances with status -2 (flagged by the fast kernel, or by
+// the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set.
 template <int NP, int M0>
 __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
 {
@@ -369,46 +420,22 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
         const long e = e0 + sub;
         const bool valid = e < cnt;
         const long b = valid ? a.wl[a.B + e] : 0;
-        const int n = a.n;
-        const bool row = valid && i < n;
-        const double h_i = row ? a.h[b * n + i] : 0.0;
         WBQ_STAMP(8);
         __syncthreads(); // the previous instance's LDS is dead
-        const bool warm = valid && a.ws_hint[b] != 0;
-        const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, valid,
-                                                   row ? a.tau_min[i] - h_i : -kInf, row ? a.tau_max[i] - h_i : kInf,
-                                                   warm);
-        WBQ_STAMP(11);
-        int status = ro.status, iters = 0;
-        bool infeasible = false;
-        // level 1 over a single feasible point needs no active set (rollouts do: they integrate
-        // u = M^-1 x, which the active set leaves in LDS)
-        const bool uniq = ro.unique && !a.integrate;
-        double x_i = ro.x;
-        if (__any(valid && !uniq))
-            x_i = gi_solve<NP, M0>(a, S, b, i, row, valid && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
-                                   infeasible);
-        if (uniq) x_i = ro.x;
-        WBQ_STAMP(12);
-#ifdef WBQ_STAMPS
-        if (threadIdx.x == 0 && a.stamps) { // step counts of the diagnostic build
-            a.stamps[blockIdx.x * kStamps + 13] = (unsigned long long)ro.it;
-            a.stamps[blockIdx.x * kStamps + 14] = (unsigned long long)iters;
-        }
-#endif
-        if (infeasible && status == 0) status = 2;
-        double tau_i = x_i + h_i;
-        if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
-        if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
-        if (row) a.tau[b * n + i] = tau_i;
-        rollout_step(a, b, i, row, S[L.U + i], status == 0);
-        if (valid && i == 0) {
-            a.status[b] = status;
-            a.iters[b] = iters + ro.it;
-            a.ws_hint[b] = ro.l0inf ? 1 : 0;
-        }
+        repair_instance<NP, M0>(a, S, b, i, valid);
     }
 }
+
+// n <= 32 with up to 6 level-0 rows: the level-0 repair is a call inside the fast kernel (one
+// launch per solve). With 12 rows the call's frame costs the fast kernel its occupancy
+// (2 -> 1 waves per SIMD), so that variant keeps the follow-up repair kernel.
+#ifdef WBQ_NO_INLINE_REPAIR
+template <int NP, int M0>
+constexpr bool kInlineRepair = false;
+#else
+template <int NP, int M0>
+constexpr bool kInlineRepair = NP == 32 && M0 <= 6;
+#endif
 
 // ====================================================================== fast path
 // An instance whose equality-constrained optimum violates a bound needs the dual active
@@ -431,6 +458,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const bool row = valid && i < n;
     const long bn = valid ? b * n : 0;
     const int ic = i < n ? i : n - 1; // clamped column for unconditional loads
+    WBQ_RTSTAMP(16);
     WBQ_STAMP(0);
 
     // ---------------------------------------------------------------- 1. stage
@@ -498,6 +526,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
         S[L.F + i] = F;
     }
+    WBQ_STAMP(15);
     // M (still streaming in during the forces): padding rows/columns past n -> identity
 #pragma unroll
     for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
@@ -693,23 +722,26 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
             int st2 = 0, it2 = 0;
             bool inf = false;
             const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf);
-            if (active) {
-                if (inf || to_rep) {
-                    if (i == 0) {
-                        a.status[b] = -2;
-                        wl_push(a, 1, b);
-                    }
-                } else {
-                    double tau2 = x2 + h_i;
-                    if (!isfinite(tau2) && st2 == 0) st2 = 3;
-                    if (st2 != 0) tau2 = h_i;
-                    if (row) a.tau[bn + i] = tau2;
-                    rollout_step(a, b, i, row, S[LA.U + i], st2 == 0);
-                    if (i == 0) {
-                        a.status[b] = st2;
-                        a.iters[b] = it2;
-                    }
+            const bool rep = active && (inf || to_rep);
+            if (active && !rep) { // (before the repair below, which reuses the wave's LDS)
+                double tau2 = x2 + h_i;
+                if (!isfinite(tau2) && st2 == 0) st2 = 3;
+                if (st2 != 0) tau2 = h_i;
+                if (row) a.tau[bn + i] = tau2;
+                rollout_step(a, b, i, row, S[LA.U + i], st2 == 0);
+                if (i == 0) {
+                    a.status[b] = st2;
+                    a.iters[b] = it2;
                 }
+            }
+            if constexpr (kInlineRepair<NP, M0>) {
+                if (__any(rep)) { // the level-0 repair right here (wave-uniform branch)
+                    __syncthreads();
+                    repair_instance<NP, M0>(a, S, b, i, rep);
+                }
+            } else if (rep && i == 0) {
+                a.status[b] = -2; // qppvm_repair_kernel
+                wl_push(a, 1, b);
             }
         } else if (active) { // park (u, Q1) for the active-set kernel
             double *us = a.u_scr + b * NP;
@@ -725,6 +757,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         }
     }
     WBQ_STAMP(5);
+    WBQ_RTSTAMP(17);
 }
 
 template <int NP, typename Lay, typename K>
@@ -753,9 +786,18 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     // follow-up kernels: grid-stride over their work lists, at most kFollowGrid blocks
     const unsigned fgrid = grid < kFollowGrid ? grid : kFollowGrid;
-    if constexpr (!MERGED) e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream);
-    if (e != hipSuccess) return e;
-    return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
+    if constexpr (kInlineRepair<NP, M0>) {
+        // active set and level-0 repair run inside the fast kernel: one launch per solve, the
+        // work lists are unused
+        (void)fgrid;
+        return hipSuccess;
+    } else if constexpr (MERGED) {
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
+    } else {
+        e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream);
+        if (e != hipSuccess) return e;
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
+    }
 }
 
 }  // namespace

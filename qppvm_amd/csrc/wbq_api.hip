@@ -661,6 +661,20 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
     return WBQ_SUCCESS;
 }
 
+int wbq_get_warmstart_hints(wbq_ctx *c, uint8_t *hints)
+{
+    if (!c || !hints) return WBQ_E_INVALID;
+    if (c->batch == 0) return WBQ_SUCCESS;
+    if (!c->ws_hint) {
+        std::memset(hints, 0, (size_t)c->batch);
+        return WBQ_SUCCESS;
+    }
+    WBQ_HIP(hipSetDevice(c->device));
+    WBQ_HIP(hipMemcpyAsync(hints, c->ws_hint, (size_t)c->batch, hipMemcpyDeviceToHost, c->stream));
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    return WBQ_SUCCESS;
+}
+
 int wbq_set_timing(wbq_ctx *c, int enable)
 {
     if (!c) return WBQ_E_INVALID;

@@ -46,9 +46,20 @@ def _pose(R, p):
     return out.reshape(R.shape[:-2] + (12,))
 
 
+# The physically scaled variant (``plant=True``): M eigenvalues in [0.5, 5] and Jacobian entries
+# N(0, 0.2^2), i.e. lever arms of ~0.2 m and an operational-space inverse inertia J M^-1 J^T of
+# O(1). The SURVEY distribution (J ~ N(0, 0.5^2), lambda(M) down to 1e-2) puts dt * Dc *
+# lambda_max(J M^-1 J^T) at ~10-100 for the reference gains (Dc = 70) at 1 kHz: explicit Euler
+# rollouts of it diverge within a few steps (config 4); the plant variant keeps it below 2.
+PLANT_LAM_LO, PLANT_COND, PLANT_JSCALE = 0.5, 10.0, 0.2
+
+
 def qppvm_instances(prob: QPPVMProblem, B: int, seed: int = 0, offset: int = 0,
-                    cond_max: float = 1e3) -> dict:
+                    cond_max: float = 1e3, plant: bool = False) -> dict:
     """B independent random instances (rows [offset, offset+B) of stream ``seed``)."""
+    lam_lo, jscale = (PLANT_LAM_LO, PLANT_JSCALE) if plant else (1e-2, 0.5)
+    if plant:
+        cond_max = PLANT_COND
     n, T = prob.n, prob.ntasks
     out = {k: [] for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
     # generate in chunks keyed by absolute chunk index so offsets are reproducible
@@ -57,10 +68,10 @@ def qppvm_instances(prob: QPPVMProblem, B: int, seed: int = 0, offset: int = 0,
     for c in range(first, last + 1):
         rng = _rng(seed, c)
         Q = _haar(rng, CH, n)
-        lam = np.exp(rng.uniform(np.log(1e-2), np.log(1e-2 * cond_max), (CH, n)))
+        lam = np.exp(rng.uniform(np.log(lam_lo), np.log(lam_lo * cond_max), (CH, n)))
         M = (Q * lam[:, None, :]) @ Q.transpose(0, 2, 1)
         M = 0.5 * (M + M.transpose(0, 2, 1))
-        J = rng.normal(0.0, 0.5, (CH, T, 6, n))
+        J = rng.normal(0.0, jscale, (CH, T, 6, n))
         R = _haar(rng, CH * T, 3).reshape(CH, T, 3, 3)
         det = np.linalg.det(R)
         R[det < 0, :, 0] *= -1.0

@@ -25,7 +25,7 @@ EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_s
            "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
            "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail", "wbq_rollout",
-           "wbq_get_state", "wbq_set_state")
+           "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints")
 
 
 class WbqError(RuntimeError):
@@ -106,11 +106,12 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_rollout.argtypes = [P, I, ctypes.c_double]
     lib.wbq_get_state.argtypes = [P, P, P]
     lib.wbq_set_state.argtypes = [P, P, P, I]
+    lib.wbq_get_warmstart_hints.argtypes = [P, P]
     for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
               "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
               "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
               "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail",
-              "wbq_rollout", "wbq_get_state", "wbq_set_state"):
+              "wbq_rollout", "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib
@@ -244,6 +245,14 @@ class QPPVMSolver:
             raise ValueError(f"mask must have one entry per instance of the batch ({self.batch}), got {m.shape}")
         self._check(self.lib.wbq_reset_warmstart(self.ctx, None if m is None else _ptr(m)),
                     "wbq_reset_warmstart")
+
+    def warm_hints(self) -> np.ndarray:
+        """Per-instance warm-start hints of the current batch (1 = the last solve went through
+        the level-0 repair with level 0 infeasible at b0)."""
+        out = np.zeros(self.batch, dtype=np.uint8)
+        if self.batch:
+            self._check(self.lib.wbq_get_warmstart_hints(self.ctx, _ptr(out)), "wbq_get_warmstart_hints")
+        return out
 
     # -- timing (HIP events around every launch, on the launch stream)
     def set_timing(self, enable: bool, every: int = 1):

@@ -14,7 +14,7 @@ run() { # name, timeout, cmd...
   echo "rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   return $rc
 }
-run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ; rc=$?
+run pytest_gpu 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$?
 if [ $rc -ge 2 ]; then echo "pytest crashed/timed out ($rc): stopping"; exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench 400 python bench.py --steps 200 --warmup 20 || exit 1
@@ -23,7 +23,8 @@ if [ "$STEPS" = "all" ]; then
   run bench_contact_cfg2 300 python bench.py --form contact --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
   run bench_w1m 300 python bench.py --weight M --steps 100 --warmup 10 --no-cpu --no-variant || exit 1
   run bench_w1m_cfg2 300 python bench.py --weight M --config 2 --steps 50 --warmup 5 --no-cpu --no-pmc --no-variant || exit 1
-  run bench_cfg4 300 python bench.py --config 4 --steps 5 --warmup 1 --no-cpu --no-pmc --no-variant || exit 1
+  run bench_cfg4 300 python bench.py --config 4 --steps 20 --warmup 2 --cpu-seconds 10 --no-variant || exit 1
+  run bench_cfg4_survey 300 python bench.py --config 4 --mpc-inputs survey --steps 5 --warmup 1 --no-cpu --no-pmc --no-variant || exit 1
   cd /tmp && run_dir="$GRAFT_REPO_ROOT/gpurun_out/prof"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$run_dir" -o run --output-format csv -- \
       python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu --no-pmc > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
@@ -31,6 +32,7 @@ if [ "$STEPS" = "all" ]; then
 fi
 if [ "$STEPS" = "all" ] || [ "$STEPS" = "plugin" ]; then
   cd "$GRAFT_REPO_ROOT"
-  run dummy_driver 300 ./qppvm_amd/qppvm_dummy_driver --ticks 10000 --dump gpurun_out/dummy_dump.bin 50 || exit 1
+  run dummy_driver 300 ./qppvm_amd/qppvm_dummy_driver --ticks 10000 || exit 1
+  run dummy_driver_stress 300 ./qppvm_amd/qppvm_dummy_driver --ticks 10000 --stress || exit 1
   run dummy_driver_forceacc 300 ./qppvm_amd/qppvm_dummy_driver --plugin forceacc --ticks 10000 || exit 1
 fi
