@@ -193,6 +193,48 @@ void wbq_destroy(wbq_ctx *ctx);
 const char *wbq_last_error(const wbq_ctx *ctx);
 const char *wbq_version(void);
 
+/* ---------------------------------------------------------------- rigid-body dynamics
+ * Batched model quantities the hot path consumes, from (q, qd) on the device. They replace the
+ * XBotInterface ModelInterface calls of the reference (RBDL backend [upstream]):
+ *   getInertiaMatrix      -> M       (used by every task, QPPVMPlugin.cpp:114-118,139,151)
+ *   computeNonlinearTerm  -> h       (QPPVMPlugin.cpp:65,312; ForceAcc.cpp:208-217 via ID)
+ *   getPose / getJacobian -> pose, J (QPPVMPlugin.cpp:272-284 and the Cartesian tasks :129-152)
+ * Model: a kinematic tree of n <= 64 revolute joints, one per link, parent[i] < i (-1 = fixed
+ * base); link i's frame is its joint frame, T_i = X_fixed[i] * Rot(axis[i], q_i) in the parent
+ * link frame. Outputs use the wbq_inputs layouts (M [B][n][n], h [B][n], J [B][T][6][n] with rows
+ * [linear; angular] of the task link's origin in the world frame, pose [B][T][12] = [R | p]), so
+ * they feed wbq_set_inputs directly (WBQ_MEM_DEVICE) or wbq_rollout_rbd. */
+typedef struct wbq_rbd_desc {
+    int n;
+    const int32_t *parent;  /* [n] */
+    const double *X_fixed;  /* [n][12] [R | p] row-major, joint frame in the parent link frame at q = 0 */
+    const double *axis;     /* [n][3] unit joint axis, joint frame */
+    const double *mass;     /* [n] */
+    const double *com;      /* [n][3] link frame */
+    const double *inertia;  /* [n][6] Ixx, Iyy, Izz, Ixy, Ixz, Iyz about the COM, link frame */
+    double gravity[3];      /* world, e.g. {0, 0, -9.81} */
+    int ntasks;             /* <= 4: the Cartesian task links (their frame origins) */
+    const int32_t *task_link;
+    int max_batch;
+} wbq_rbd_desc;
+
+typedef struct wbq_rbd_ctx wbq_rbd_ctx;
+
+int wbq_rbd_create(const wbq_rbd_desc *desc, int device, wbq_rbd_ctx **out);
+/* One launch over `batch` instances on the context's stream (asynchronous; all pointers of the
+ * same memory kind: WBQ_MEM_DEVICE pointers are used in place, WBQ_MEM_HOST ones are staged and
+ * the call waits for the outputs). Any output may be NULL. */
+int wbq_rbd_compute(wbq_rbd_ctx *ctx, int batch, const double *q, const double *qd, double *M, double *h,
+                    double *J, double *pose, int memory);
+int wbq_rbd_set_stream(wbq_rbd_ctx *ctx, void *hip_stream);
+void wbq_rbd_destroy(wbq_rbd_ctx *ctx);
+/* MPC rollouts with the model re-evaluated every step: per step, M, h, J and
+ * poses of the QPPVM context's inputs are recomputed from its integrated q, qd, then one solve
+ * integrates them (wbq_rollout). The QPPVM context must hold device-resident inputs of its own
+ * (set with WBQ_MEM_HOST, or WBQ_MEM_DEVICE buffers the caller lets it overwrite) and n, ntasks
+ * equal to the model's; both contexts on one device. */
+int wbq_rollout_rbd(wbq_ctx *ctx, wbq_rbd_ctx *rbd, int steps, double dt);
+
 #ifdef __cplusplus
 }
 #endif

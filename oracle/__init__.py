@@ -15,7 +15,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
-SRCS = [os.path.join(HERE, f) for f in ("wbq_oracle.c", "wbq_oracle_contact.c")]
+SRCS = [os.path.join(HERE, f) for f in ("wbq_oracle.c", "wbq_oracle_contact.c", "wbq_oracle_rbd.c")]
 
 
 def build(force: bool = False) -> str:
@@ -65,6 +65,10 @@ def lib():
         _lib.wbq_ref_contact_one.argtypes = [P, P, P, P, P, P]
         _lib.wbq_ref_contact_one.restype = I
         _lib.wbq_ref_contact_batch.argtypes = [P, I] + [P] * 14 + [P, P, P, P, P]
+        _lib.wbq_ref_rbd_one.argtypes = [P] * 7
+        _lib.wbq_ref_rbd_one.restype = None
+        _lib.wbq_ref_rnea.argtypes = [P] * 5
+        _lib.wbq_ref_rnea.restype = None
     return _lib
 
 
@@ -245,3 +249,47 @@ def contact_batch(prob, inputs):
     lib().wbq_ref_contact_batch(ctypes.byref(d), B, *[_p(a) for a in arrs], _p(cm), _p(tau), _p(x), _p(st),
                                 _p(it), _p(rep))
     return tau, x, st, it, rep
+
+
+# ---------------------------------------------------------------- rigid-body dynamics
+class _RbdModel(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("parent", ctypes.c_void_p), ("X_fixed", ctypes.c_void_p),
+                ("axis", ctypes.c_void_p), ("mass", ctypes.c_void_p), ("com", ctypes.c_void_p),
+                ("inertia", ctypes.c_void_p), ("gravity", ctypes.c_double * 3), ("ntasks", ctypes.c_int),
+                ("task_link", ctypes.c_void_p)]
+
+
+def _rbd_model(model):
+    """model: qppvm_amd.rbd.RobotModel (or any object with its fields)."""
+    keep = {k: np.ascontiguousarray(getattr(model, k), dtype=np.int32 if k in ("parent", "task_link") else np.float64)
+            for k in ("parent", "X_fixed", "axis", "mass", "com", "inertia", "task_link")}
+    m = _RbdModel()
+    m.n = int(model.n)
+    for k, v in keep.items():
+        setattr(m, k, v.ctypes.data)
+    m.gravity = (ctypes.c_double * 3)(*[float(g) for g in model.gravity])
+    m.ntasks = int(len(keep["task_link"]))
+    return m, keep
+
+
+def rbd_batch(model, q, qd):
+    """M [B][n][n], h [B][n], J [B][T][6][n], pose [B][T][12] for each (q, qd) row."""
+    L = lib()
+    m, keep = _rbd_model(model)
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+    qd = np.ascontiguousarray(np.atleast_2d(qd), dtype=np.float64)
+    B, n, T = q.shape[0], model.n, len(model.task_link)
+    M = np.zeros((B, n, n)); h = np.zeros((B, n)); J = np.zeros((B, T, 6, n)); pose = np.zeros((B, T, 12))
+    for b in range(B):
+        L.wbq_ref_rbd_one(ctypes.byref(m), _p(q[b]), _p(qd[b]), _p(M[b]), _p(h[b]), _p(J[b]), _p(pose[b]))
+    return M, h, J, pose
+
+
+def rnea(model, q, qd, qdd):
+    L = lib()
+    m, keep = _rbd_model(model)
+    tau = np.zeros(model.n)
+    L.wbq_ref_rnea(ctypes.byref(m), _p(np.ascontiguousarray(q, dtype=np.float64)),
+                   _p(np.ascontiguousarray(qd, dtype=np.float64)), _p(np.ascontiguousarray(qdd, dtype=np.float64)),
+                   _p(tau))
+    return tau

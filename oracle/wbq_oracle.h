@@ -161,6 +161,30 @@ void wbq_ref_contact_batch(const wbq_ref_contact_desc *d, int B, const double *M
                            const double *pose_c, const double *pose_c_ref, const int32_t *cmask, double *tau,
                            double *x, int32_t *status, int32_t *iters, int32_t *l0_repaired);
 
+/* ---- rigid-body dynamics (oracle/wbq_oracle_rbd.c): kinematic tree of revolute joints, one
+ * per link, parent[i] < i (-1 = fixed base); link frame = joint frame,
+ * T_i = X_fixed[i] Rot(axis[i], q_i) in the parent link frame. Same fields as wbq_rbd_desc
+ * (include/wbq.h). */
+#define WBQ_REF_RBD_MAX 64
+typedef struct {
+    int n;
+    const int *parent;      /* [n] */
+    const double *X_fixed;  /* [n][12] [R | p] row-major */
+    const double *axis;     /* [n][3] unit, joint frame */
+    const double *mass;     /* [n] */
+    const double *com;      /* [n][3] link frame */
+    const double *inertia;  /* [n][6] Ixx Iyy Izz Ixy Ixz Iyz about the COM, link frame */
+    double gravity[3];
+    int ntasks;
+    const int *task_link;   /* [ntasks] */
+} wbq_ref_rbd_model;
+
+void wbq_ref_rnea(const wbq_ref_rbd_model *m, const double *q, const double *qd, const double *qdd, double *tau);
+void wbq_ref_crba(const wbq_ref_rbd_model *m, const double *q, double *M);
+void wbq_ref_link_kinematics(const wbq_ref_rbd_model *m, const double *q, int e, double *pose, double *J);
+void wbq_ref_rbd_one(const wbq_ref_rbd_model *m, const double *q, const double *qd, double *M, double *h,
+                     double *J, double *pose);
+
 #ifdef __cplusplus
 }
 #endif

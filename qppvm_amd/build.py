@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwbq.so")
-SOURCES = ["wbq_api.hip", "qppvm_kernel.hip", "qppvm_w1m_kernel.hip", "contact_kernel.hip"]
+SOURCES = ["wbq_api.hip", "qppvm_kernel.hip", "qppvm_w1m_kernel.hip", "contact_kernel.hip", "rbd.hip"]
 HEADERS = ["wbq_kernels.h", "wbq_device.h", "dual_gi.h", "qppvm_repair.h"]
 ARCH = os.environ.get("WBQ_ARCH", "gfx950")
 

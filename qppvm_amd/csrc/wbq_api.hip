@@ -558,6 +558,30 @@ int wbq_rollout(wbq_ctx *c, int steps, double dt)
     return WBQ_SUCCESS;
 }
 
+int wbq_rollout_rbd(wbq_ctx *c, wbq_rbd_ctx *rbd, int steps, double dt)
+{
+    if (!c || !rbd) return WBQ_E_INVALID;
+    if (c->form != WBQ_FORM_QPPVM) return fail(c, WBQ_E_UNSUPPORTED, "wbq_rollout_rbd: QPPVM form only");
+    if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
+    if (wbq::rbd_n(rbd) != c->d.n || wbq::rbd_ntasks(rbd) != c->d.ntasks || wbq::rbd_device(rbd) != c->device)
+        return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: model n / ntasks / device differ from the context's");
+    if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: steps >= 0, dt >= 0");
+    WBQ_HIP(hipSetDevice(c->device));
+    if (c->in_pending && c->in_stream != c->stream) {
+        WBQ_HIP(hipStreamWaitEvent(c->stream, c->in_copied, 0));
+        c->in_stream = c->stream;
+    }
+    // the model is re-evaluated in place at the integrated state, then one integrating solve
+    double *M = const_cast<double *>(c->in[0]), *J = const_cast<double *>(c->in[1]);
+    double *pose = const_cast<double *>(c->in[2]), *h = const_cast<double *>(c->in[7]);
+    for (int k = 0; k < steps; ++k) {
+        WBQ_HIP(wbq::rbd_launch(rbd, c->batch, c->in[4], c->in[5], M, h, J, pose, c->stream));
+        const int rc = solve_impl(c, 1, dt);
+        if (rc != WBQ_SUCCESS) return rc;
+    }
+    return WBQ_SUCCESS;
+}
+
 int wbq_get_state(wbq_ctx *c, double *q, double *qd)
 {
     if (!c) return WBQ_E_INVALID;

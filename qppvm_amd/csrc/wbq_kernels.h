@@ -116,6 +116,20 @@ __device__ __forceinline__ void rollout_step(const Args &a, long b, int i, bool 
 // mid (optional): recorded right after the main kernel, before the level-0 repair kernel
 hipError_t launch_contact(const ContactArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 
+}  // namespace wbq
+
+struct wbq_rbd_ctx; // rbd.hip
+
+namespace wbq {
+
+// Batched rigid-body quantities (rbd.hip): one launch over B instances, outputs in the wbq input
+// layouts (any may be null).
+hipError_t rbd_launch(const wbq_rbd_ctx *c, int B, const double *q, const double *qd, double *M, double *h, double *J,
+                      double *pose, hipStream_t stream);
+int rbd_n(const wbq_rbd_ctx *c);
+int rbd_ntasks(const wbq_rbd_ctx *c);
+int rbd_device(const wbq_rbd_ctx *c);
+
 // Lanes per instance used for a given n (32 for n <= 32, else 64).
 inline int lanes_per_instance(int n) { return n <= 32 ? 32 : 64; }
 

@@ -25,7 +25,8 @@ EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_s
            "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs", "wbq_reset_warmstart", "wbq_set_timing",
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
            "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail", "wbq_rollout",
-           "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints")
+           "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints", "wbq_rbd_create", "wbq_rbd_compute",
+           "wbq_rbd_set_stream", "wbq_rbd_destroy", "wbq_rollout_rbd")
 
 
 class WbqError(RuntimeError):
@@ -107,11 +108,18 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_get_state.argtypes = [P, P, P]
     lib.wbq_set_state.argtypes = [P, P, P, I]
     lib.wbq_get_warmstart_hints.argtypes = [P, P]
+    lib.wbq_rbd_create.argtypes = [P, I, ctypes.POINTER(P)]
+    lib.wbq_rbd_compute.argtypes = [P, I, P, P, P, P, P, P, I]
+    lib.wbq_rbd_set_stream.argtypes = [P, P]
+    lib.wbq_rbd_destroy.argtypes = [P]
+    lib.wbq_rbd_destroy.restype = None
+    lib.wbq_rollout_rbd.argtypes = [P, P, I, ctypes.c_double]
     for f in ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_sync",
               "wbq_get_outputs", "wbq_set_outputs", "wbq_get_device_outputs",
               "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
               "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail",
-              "wbq_rollout", "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints"):
+              "wbq_rollout", "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints", "wbq_rbd_create",
+              "wbq_rbd_compute", "wbq_rbd_set_stream", "wbq_rollout_rbd"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib
@@ -245,6 +253,11 @@ class QPPVMSolver:
             raise ValueError(f"mask must have one entry per instance of the batch ({self.batch}), got {m.shape}")
         self._check(self.lib.wbq_reset_warmstart(self.ctx, None if m is None else _ptr(m)),
                     "wbq_reset_warmstart")
+
+    def rollout_rbd(self, rbd, steps: int, dt: float):
+        """MPC rollout with M, h, J and poses re-evaluated on the device every step from the
+        integrated state (``rbd``: qppvm_amd.rbd.RBDModel on the same device)."""
+        self._check(self.lib.wbq_rollout_rbd(self.ctx, rbd.ctx, int(steps), float(dt)), "wbq_rollout_rbd")
 
     def warm_hints(self) -> np.ndarray:
         """Per-instance warm-start hints of the current batch (1 = the last solve went through
