@@ -72,6 +72,26 @@ def build_workload(form, config, n, B, world, rank, device, weight=0, global_bat
     from qppvm_amd.wbq import ContactSolver, QPPVMSolver
     plan = shard_plan(config, B, world, global_batch)
     B = plan.count(rank)
+    if config == 4 and form == "qppvm" and plant == "rbd":
+        # MPC on a model: M, h, J, poses of a humanoid-like tree (qppvm_amd/rbd.py) from its
+        # state, re-evaluated on the device every rollout step (wbq_rollout_rbd)
+        from qppvm_amd.rbd import RBDModel, centauro_like, humanoid_like
+        model = centauro_like() if n == 39 else humanoid_like(n)
+        rng = np.random.default_rng(1000 + rank)
+        q0, qd0 = rng.uniform(-0.5, 0.5, (B, n)), rng.normal(0.0, 0.5, (B, n))
+        r = RBDModel(model, max_batch=B, device=device)
+        M, h, J, pose = r.compute(q0, qd0)
+        r.close()
+        pref = pose.copy()
+        pref[:, :, [3, 7, 11]] += rng.normal(0.0, 0.02, (B, model.ntasks, 3))
+        inp = dict(M=M, J=J, pose=pose, pose_ref=pref, q=q0, qd=qd0, qref=q0.copy(), h=h)
+        free = QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9, joint_weight=weight), max_batch=B, device=device)
+        tau_free, _, _ = free.solve_batch(inp)
+        free.close()
+        prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)), joint_weight=weight)
+        prob.rbd_model = model
+        return prob, inp, QPPVMSolver
+    plant = plant is True
     if config in (3, 4):
         config = 2  # config 3 shards and MPC rollouts start from the config-2 random states
     if form == "qppvm":
@@ -169,9 +189,14 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         churn = dict(live=live, alt=alt, calls=0, slice=(B + 4) // 5)
         torch.cuda.synchronize()
 
+    rbd = None
     if config == 4:  # each MPC step re-plans from the measured state: a D2D reset of (q, qd)
         q0 = torch.from_numpy(np.ascontiguousarray(inp["q"])).to(f"cuda:{device}")
         qd0 = torch.from_numpy(np.ascontiguousarray(inp["qd"])).to(f"cuda:{device}")
+        if getattr(prob, "rbd_model", None) is not None:
+            from qppvm_amd.rbd import RBDModel
+            rbd = RBDModel(prob.rbd_model, max_batch=B, device=device)
+            rbd.set_stream(None)
         torch.cuda.synchronize()
 
     def step():
@@ -189,7 +214,10 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
             churn["calls"] = c + 1
         if config == 4:
             solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
-            solver.rollout(HORIZON, MPC_DT)
+            if rbd is not None:
+                solver.rollout_rbd(rbd, HORIZON, MPC_DT)
+            else:
+                solver.rollout(HORIZON, MPC_DT)
         else:
             solver.solve()
         if gather_buf is not None:
@@ -237,12 +265,19 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
         shares = []
         for _ in range(HORIZON):
-            solver.rollout(1, MPC_DT)
+            if rbd is not None:
+                solver.rollout_rbd(rbd, 1, MPC_DT)
+            else:
+                solver.rollout(1, MPC_DT)
             shares.append(float(solver.warm_hints().mean()))
         mpc = {"repair_share_per_step": float(np.mean(shares)), "repair_share_last_step": shares[-1],
                "euler_dt_Dc_lambda_max": euler_stability(prob, inp, MPC_DT),
-               "inputs": "plant-scaled (lambda(M) in [0.5, 5], J ~ N(0, 0.2^2))" if plant else
-                         "SURVEY 8d distribution (lambda(M) in [1e-2, 1e1], J ~ N(0, 0.5^2))"}
+               "inputs": ("on-device rigid-body model re-evaluated every step (wbq_rollout_rbd), "
+                          f"{prob.rbd_model.n}-joint tree" if rbd is not None else
+                          "plant-scaled (lambda(M) in [0.5, 5], J ~ N(0, 0.2^2))" if plant else
+                          "SURVEY 8d distribution (lambda(M) in [1e-2, 1e1], J ~ N(0, 0.5^2))")}
+        if rbd is not None:
+            rbd.close()
     if gather_buf is not None:  # the gathered tau holds this rank's shard where the plan puts it
         g = gather_buf[rank * plan.max_count: rank * plan.max_count + B].cpu().numpy()
         assert np.array_equal(g, tau), "all-gathered tau differs from the rank's own solve"
@@ -321,14 +356,18 @@ def cpu_baseline(form, prob, inp, budget_s):
 
 def cpu_baseline_mpc(prob, inp, budget_s, rollouts=32):
     """Config 4 on the CPU: the oracle solves each step of a bounded sample of rollouts, numpy
-    integrates (q_dd = M^-1 (tau - h), semi-implicit Euler), HORIZON steps per rollout."""
+    integrates (q_dd = M^-1 (tau - h), semi-implicit Euler), HORIZON steps per rollout (with a
+    model: the oracle's recursions re-evaluate it every step)."""
     import oracle
     oracle.build()
+    model = getattr(prob, "rbd_model", None)
     done, t0, B = 0, time.perf_counter(), inp["h"].shape[0]
     while time.perf_counter() - t0 < budget_s:
         lo = (done // HORIZON) % B
         cur = {k: v[lo:lo + rollouts].copy() for k, v in inp.items()}
         for _ in range(HORIZON):
+            if model is not None:
+                cur["M"], cur["h"], cur["J"], cur["pose"] = oracle.rbd_batch(model, cur["q"], cur["qd"])
             tau, st, _ = oracle.qppvm_batch(prob, cur)
             qdd = np.linalg.solve(cur["M"], (tau - cur["h"])[..., None])[..., 0]
             qdd[st != 0] = 0.0
@@ -412,9 +451,10 @@ def main():
                          "3: a fixed global batch of random states sharded over the GPUs + all-gather of tau; "
                          "4: MPC, each step = HORIZON sequential solves per rollout (wbq_rollout)")
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of tau per step (config 3: always)")
-    ap.add_argument("--mpc-inputs", choices=("plant", "survey"), default="plant",
-                    help="config 4 states: plant-scaled (stable explicit Euler at the reference gains, default) "
-                         "or the SURVEY 8d distribution (its rollouts diverge into level-0 repairs)")
+    ap.add_argument("--mpc-inputs", choices=("plant", "survey", "rbd"), default="plant",
+                    help="config 4 states: plant-scaled (stable explicit Euler at the reference gains, default), "
+                         "the SURVEY 8d distribution (its rollouts diverge into level-0 repairs), or a rigid-body "
+                         "model re-evaluated on the device every step (wbq_rollout_rbd)")
     ap.add_argument("--weight", choices=("I", "M"), default="I", help="QPPVM joint-task weight W1 (SURVEY 8a a6)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -452,7 +492,7 @@ def main():
     n, B = args.n, args.batch
     weight = 1 if args.weight == "M" else 0
     kern = dominant_kernel(args.form, weight)
-    plant = args.config == 4 and args.mpc_inputs == "plant"
+    plant = ("rbd" if args.mpc_inputs == "rbd" else args.mpc_inputs == "plant") if args.config == 4 else False
     m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, allgather, dist,
             args.host_io, weight, args.global_batch, plant)
     value = m["total"] / m["dt"]
@@ -471,6 +511,10 @@ def main():
           ("qppvm", 4): f"MPC: rollouts x N={HORIZON} sequential QPPVM QPs, on-device semi-implicit Euler "
                         "(dt=1e-3), J/M/h frozen, warm-start carry (config 4)",
           ("contact", 4): f"MPC: rollouts x N={HORIZON} sequential contact-form QPs, on-device Euler (config 4)"}
+    if args.config == 4 and args.mpc_inputs == "rbd":
+        wl[("qppvm", 4)] = (f"MPC: rollouts x N={HORIZON} sequential QPPVM QPs, M/h/J/poses re-evaluated on the device "
+                            "every step from the integrated state (rigid-body model, wbq_rollout_rbd), semi-implicit "
+                            "Euler (dt=1e-3), warm-start carry (config 4)")
     per_gpu = f"batch={m['B_local']}/GPU" if args.config != 3 else f"global batch={args.global_batch}"
     st, it = m["status"], m["iters"]
     line = {

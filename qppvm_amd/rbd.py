@@ -92,6 +92,28 @@ def centauro_like(seed=7) -> RobotModel:
     return random_tree(parent, seed=seed, task_link=(14, 7), names=names)
 
 
+def humanoid_like(n=30, seed=5) -> RobotModel:
+    """A floating-base-free humanoid-like tree of n >= 16 joints: a torso chain on the fixed
+    pelvis, two 7-DoF arms on the torso top, the remaining joints as two legs on the pelvis.
+    Tasks on the two arm ends (right first, as QPPVMPlugin's stack)."""
+    if n < 16:
+        raise ValueError("humanoid_like needs n >= 16")
+    legs = n - 14 - 2
+    parent, names = [-1, 0], ["torso_1", "torso_2"]
+    ends = []
+    for arm in (1, 2):
+        for j in range(7):
+            parent.append(1 if j == 0 else len(parent) - 1)
+            names.append(f"arm{arm}_{j + 1}")
+        ends.append(len(parent) - 1)
+    for leg in range(2):
+        cnt = legs // 2 + (leg < legs % 2)
+        for j in range(cnt):
+            parent.append(-1 if j == 0 else len(parent) - 1)
+            names.append(f"leg{leg + 1}_{j + 1}")
+    return random_tree(parent, seed=seed, task_link=(ends[1], ends[0]), names=names)
+
+
 def serial_chain(n=30, seed=3, ntasks=2) -> RobotModel:
     """A serial chain (depth n) with tasks on the last link and the middle link."""
     parent = [-1] + list(range(n - 1))
