@@ -88,27 +88,16 @@ template <int NP>
 __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> &L, double npj, int q, int i)
 {
     constexpr int RS = NP + 1;
-    double d1 = 0.0;
-    if (i < q) {
-#pragma unroll
-        for (int j = 0; j < NP; ++j) d1 = fma(S[L.QA + i * RS + j], S[L.NV + j], d1);
-    }
+    const double d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
     S[L.D1 + i] = d1;
     __syncthreads();
-    double z = npj;
-#pragma unroll
-    for (int c = 0; c < NP; ++c) z = fma(-S[L.QA + c * RS + i], S[L.D1 + c], z);
+    double z = npj - dot4s<NP>(S + L.QA + i, RS, S + L.D1);
     S[L.BC + i] = z;
     __syncthreads();
-    double d1b = 0.0;
-    if (i < q) {
-#pragma unroll
-        for (int j = 0; j < NP; ++j) d1b = fma(S[L.QA + i * RS + j], S[L.BC + j], d1b);
-    }
+    const double d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
     S[L.D1B + i] = d1b;
     __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NP; ++c) z = fma(-S[L.QA + c * RS + i], S[L.D1B + c], z);
+    z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
     S[L.D1 + i] = d1 + d1b;
     __syncthreads();
     return z;
@@ -348,9 +337,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     }
 }
 
-// Inlined into the fast kernel (n <= 32): A/B on MI355X (profiles/r02_v5_ab_*), config 1
-// 96.9 -> 107.5 M QP/s (the follow-up launch is gone); as a real call (noinline) the call
-// frame slows the whole fast kernel (89.0 M QP/s).
+// With WBQ_INLINE_REPAIR: inlined (a real call, noinline, slowed the whole fast kernel:
+// profiles/r02_v5_ab_noinline_c1.log).
 #ifndef WBQ_REPAIR_INLINE
 #define WBQ_REPAIR_INLINE __forceinline__
 #endif
@@ -426,15 +414,16 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
     }
 }
 
-// n <= 32 with up to 6 level-0 rows: the level-0 repair is a call inside the fast kernel (one
-// launch per solve). With 12 rows the call's frame costs the fast kernel its occupancy
-// (2 -> 1 waves per SIMD), so that variant keeps the follow-up repair kernel.
-#ifdef WBQ_NO_INLINE_REPAIR
-template <int NP, int M0>
-constexpr bool kInlineRepair = false;
-#else
+// The level-0 repair inside the fast kernel (n <= 32, WBQ_INLINE_REPAIR builds) saves the
+// follow-up launch but its register demand spills into the fast path: A/B on one box
+// (profiles/r02_v8_ab_*) config 1 113.7 M QP/s inlined vs 115.2 M as the separate kernel,
+// config 2 14.2 M vs 17.8 M. Off by default.
+#ifdef WBQ_INLINE_REPAIR
 template <int NP, int M0>
 constexpr bool kInlineRepair = NP == 32 && M0 <= 6;
+#else
+template <int NP, int M0>
+constexpr bool kInlineRepair = false;
 #endif
 
 // ====================================================================== fast path
@@ -442,7 +431,11 @@ constexpr bool kInlineRepair = NP == 32 && M0 <= 6;
 // set: with MERGED (NP = 32, where the active-set layout fits next to the fast one) it runs
 // right here, inline; otherwise it parks (u, Q1) in scratch for qppvm_active_kernel
 // (status -1). One whose level 0 is infeasible at b0 goes to qppvm_repair_kernel (-2).
-template <int NP, int M0, bool MERGED>
+// TM: the most tasks this instantiation handles (a.ntasks <= TM): with TM = 2 the stage issues
+// 12 J-row loads and 2 pose loads per lane instead of 24 and 3 (TM = 4), which keeps a
+// wave's stage under the 63 outstanding vector loads, and the elimination carries 3
+// right-hand sides instead of 5.
+template <int NP, int M0, bool MERGED, int TM>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -474,14 +467,14 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const unsigned char hint_b = a.ws_hint[valid ? b : 0]; // unconditional: no branch on it here
     // J and the poses first, M last: vmcnt waits are in order, so the task forces (J, poses,
     // qd) can start while M is still streaming in
-    double jv[kTMax * 6];
+    double jv[TM * 6];
     {
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.J, b0, B, (long)T * 6 * n);
         const int joff = (int)(8 * (lb * T * 6 * n + ic));
 #pragma unroll
-        for (int rr = 0; rr < kTMax * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
+        for (int rr = 0; rr < TM * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
     }
-    constexpr int kPoseIt = (kTMax * 24 + NP - 1) / NP;
+    constexpr int kPoseIt = (TM * 24 + NP - 1) / NP;
     double pv[kPoseIt];
     {
         const long base = lb * T * 12;
@@ -509,7 +502,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
 #pragma unroll
-    for (int rr = 0; rr < kTMax * 6; ++rr)
+    for (int rr = 0; rr < TM * 6; ++rr)
         if (rr < T * 6) S[L.JR + rr * NP + i] = row ? jv[rr] : 0.0;
 #pragma unroll
     for (int it = 0; it < kPoseIt; ++it)
@@ -518,9 +511,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
         const int t = i / 6, r = i - t * 6;
-        double xd = 0.0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) xd = fma(S[L.JR + i * NP + j], S[L.QD + j], xd);
+        const double xd = dot4<NP>(S + L.JR + i * NP, S + L.QD);
         const double er = cart_error_component(S + L.PS + t * 24, S + L.PS + t * 24 + 12, r);
         double F = a.Kc[i] * er - a.Dc[i] * xd;
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
@@ -547,21 +538,21 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     WBQ_STAMP(1);
 
     // ------------------------------------------ 2. block Gauss-Jordan, M SPD
-    double rhs[1 + kTMax];
+    double rhs[1 + TM];
     rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
     const double tau_imp_i = rhs[0];
 #pragma unroll
-    for (int t = 0; t < kTMax; ++t) {
+    for (int t = 0; t < TM; ++t) {
         double c = 0.0;
         if (t < T)
 #pragma unroll
             for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
         rhs[1 + t] = c; // J_t^T F_t
     }
-    bool notspd = block_gj<NP, 1 + kTMax, 8>(A, rhs, n, i, S + L.PN, S + L.RH);
+    bool notspd = block_gj<NP, 1 + TM, 8>(A, rhs, n, i, S + L.PN, S + L.RH);
     const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
 #pragma unroll
-    for (int t = 0; t < kTMax; ++t)
+    for (int t = 0; t < TM; ++t)
         if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
     __syncthreads();
     WBQ_STAMP(2);
@@ -573,10 +564,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         for (int pp = i; pp < npairs + m0; pp += NP) {
             if (pp < m0) {
                 const int rr = a.row_sel[pp], t = rr / 6;
-                double v = 0.0;
-#pragma unroll
-                for (int j = 0; j < NP; ++j) v = fma(S[L.JR + rr * NP + j], S[L.WV + t * NP + j], v);
-                S[L.RES + pp] = v;
+                S[L.RES + pp] = dot4<NP>(S + L.JR + rr * NP, S + L.WV + t * NP);
             } else {
                 const int p2 = pp - m0;
                 int ra = (int)((sqrtf(8.0f * p2 + 1.0f) - 1.0f) * 0.5f);
@@ -584,10 +572,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
                 ra -= (ra * (ra + 1) / 2 > p2) ? 1 : 0;
                 const int ca = p2 - ra * (ra + 1) / 2;
                 const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
-                double g = 0.0;
-#pragma unroll
-                for (int j = 0; j < NP; ++j) g = fma(S[L.JR + r1 * NP + j], S[L.JR + r2 * NP + j], g);
-                S[L.GR + ra * kM0Max + ca] = g;
+                S[L.GR + ra * kM0Max + ca] = dot4<NP>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
             }
         }
     }
@@ -682,9 +667,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
         __syncthreads();
         if (active && i < m0) {
             const int rr = a.row_sel[i];
-            double v = S[L.RES + i];
-#pragma unroll
-            for (int j = 0; j < NP; ++j) v = fma(S[L.JR + rr * NP + j], S[L.U + j], v);
+            const double v = S[L.RES + i] + dot4<NP>(S + L.JR + rr * NP, S + L.U);
             a.b0_scr[b * kM0Max + i] = v;
         }
     }
@@ -778,7 +761,10 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
     constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
-    hipError_t e = launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED>, a, grid, stream);
+    hipError_t e = a.ntasks <= 2
+                       ? launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED, 2>, a, grid, stream)
+                       : launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED, kTMax>, a, grid,
+                                                                   stream);
     if (e != hipSuccess) return e;
     if (mid) { // end of the dominant launch
         e = hipEventRecord(mid, stream);

@@ -116,11 +116,11 @@ struct RowStore<NP, true> {
     }
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
+        double s[4] = {0.0, 0.0, 0.0, 0.0}; // four accumulators: a shorter dependent chain
 #pragma unroll
         for (int j = 0; j < NP; ++j)
-            if (j < cnt) s = fma(v[j], b[j], s);
-        return s;
+            if (j < cnt) s[j & 3] = fma(v[j], b[j], s[j & 3]);
+        return (s[0] + s[1]) + (s[2] + s[3]);
     }
 };
 
@@ -141,6 +141,38 @@ struct RowStore<NP, false> {
         return s;
     }
 };
+
+// Dot product of two N-vectors (LDS or registers) with four independent accumulators: the
+// 32-long chains of dependent DP FMAs of the per-lane dots were latency on the critical path.
+template <int N>
+__device__ __forceinline__ double dot4(const double *a, const double *b)
+{
+    static_assert(N % 4 == 0, "dot4: N multiple of 4");
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 4) {
+        s0 = fma(a[j], b[j], s0);
+        s1 = fma(a[j + 1], b[j + 1], s1);
+        s2 = fma(a[j + 2], b[j + 2], s2);
+        s3 = fma(a[j + 3], b[j + 3], s3);
+    }
+    return (s0 + s1) + (s2 + s3);
+}
+// same with a stride on the first operand (a column of a row-major LDS matrix)
+template <int N>
+__device__ __forceinline__ double dot4s(const double *a, int stride, const double *b)
+{
+    static_assert(N % 4 == 0, "dot4s: N multiple of 4");
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 4) {
+        s0 = fma(a[j * stride], b[j], s0);
+        s1 = fma(a[(j + 1) * stride], b[j + 1], s1);
+        s2 = fma(a[(j + 2) * stride], b[j + 2], s2);
+        s3 = fma(a[(j + 3) * stride], b[j + 3], s3);
+    }
+    return (s0 + s1) + (s2 + s3);
+}
 
 template <int NP>
 __device__ __forceinline__ double isum(double v)
