@@ -367,6 +367,10 @@ template <int NQ, bool TR, int KMR, bool REPAIR>
 __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b)
 {
     constexpr int NRC = TR ? 40 : 16; // Gauss-Jordan right-hand sides per pass
+    // the most contacts this instantiation serves (KMR = 18: nc <= 2, launch_nq): the stage then
+    // issues 12 contact-Jacobian loads per lane instead of 24 (a wave's loads stay under the 63
+    // outstanding vector memory operations, as the QPPVM fast kernel's TM)
+    constexpr int CM = (!TR && KMR <= 18) ? 2 : kCMax;
     extern __shared__ __attribute__((aligned(16))) double S[];
     const int n = a.n, nc = a.nc, nf = 3 * nc;
     const ContactLayout L(n, nc, TR, NQ, NRC);
@@ -390,18 +394,18 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
         for (int r = 0; r < NQ; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     }
-    double jc[6 * kCMax], jw[6];
+    double jc[6 * CM], jw[6];
     {
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
         const int joff = (int)(8 * ic);
 #pragma unroll
-        for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = bload(Jrs, joff, 8 * (rr < 6 * nc ? rr : 6 * nc - 1) * n);
+        for (int rr = 0; rr < 6 * CM; ++rr) jc[rr] = bload(Jrs, joff, 8 * (rr < 6 * nc ? rr : 6 * nc - 1) * n);
         const __amdgpu_buffer_rsrc_t Wrs = rsrc_at(a.Jw, b, B, 6L * n);
         const int woff = (int)(8 * ic);
 #pragma unroll
         for (int r = 0; r < 6; ++r) jw[r] = bload(Wrs, woff, 8 * r * n);
     }
-    constexpr int kPoseIt = (24 * (1 + kCMax) + 63) / 64;
+    constexpr int kPoseIt = (24 * (1 + CM) + 63) / 64;
     double pv[kPoseIt];
 #pragma unroll
     for (int it = 0; it < kPoseIt; ++it) {
@@ -417,21 +421,21 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
     for (int r = 0; r < NQ; ++r) mrow[r] = (qrow && r < n) ? mrow[r] : 0.0;
 #pragma unroll
-    for (int rr = 0; rr < 6 * kCMax; ++rr) jc[rr] = (qrow && rr < 6 * nc) ? jc[rr] : 0.0;
+    for (int rr = 0; rr < 6 * CM; ++rr) jc[rr] = (qrow && rr < 6 * nc) ? jc[rr] : 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) jw[r] = qrow ? jw[r] : 0.0;
     if (i < L.NJ) { // joint constraint rows (every joint with torque rows, else the 6 base rows)
 #pragma unroll
         for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = mrow[r];
 #pragma unroll
-        for (int f = 0; f < 3 * kCMax; ++f)
+        for (int f = 0; f < 3 * CM; ++f)
             if (f < nf) S[L.FFJ + i * L.FS + f] = ((cm >> (f / 3)) & 1) ? -jc[6 * (f / 3) + f % 3] : 0.0;
     }
     if (i < NQ) {
 #pragma unroll
         for (int r = 0; r < 6; ++r) S[L.AQW + r * L.QS + i] = jw[r];
 #pragma unroll
-        for (int rr = 0; rr < 6 * kCMax; ++rr)
+        for (int rr = 0; rr < 6 * CM; ++rr)
             if (rr < 6 * nc) S[L.JC + rr * NQ + i] = jc[rr];
     }
     S[L.QD + i] = qrow ? qd_i : 0.0;
@@ -461,7 +465,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     for (int j = 0; j < NQ; ++j) A[j] = (j == i) ? 1.0 : 0.0;
     double mg = qrow ? a.Kp_p * (qref_i - q_i) - a.Kd_p * qd_i : 0.0; // -g_i = b_p + sum J_c^T b_c
 #pragma unroll
-    for (int rr = 0; rr < 6 * kCMax; ++rr) {
+    for (int rr = 0; rr < 6 * CM; ++rr) {
         if (rr < 6 * nc) {
             const double v = jc[rr];
             const double *Jr = S + L.JC + rr * NQ;
@@ -542,12 +546,12 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
     for (int j = 0; j < NQ; ++j) aq[j] = 0.0;
     if (kind != 0) {
-        double fc[3 * kCMax];
+        double fc[3 * CM];
         const double *rq = row_q(S, L, ci);
 #pragma unroll
         for (int j = 0; j < NQ; ++j) aq[j] = rq ? rq[j] : 0.0;
 #pragma unroll
-        for (int f = 0; f < 3 * kCMax; ++f) fc[f] = f < nf ? fcoef(S, L, ci, f) : 0.0;
+        for (int f = 0; f < 3 * CM; ++f) fc[f] = f < nf ? fcoef(S, L, ci, f) : 0.0;
         for (int cl = 0; cl < ME; ++cl) {
             double g = 0.0;
             if (cl < NJ + 6) {
@@ -559,12 +563,12 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
             if (cl < NJ) {
                 const double *fr = S + L.FFJ + cl * L.FS;
 #pragma unroll
-                for (int f = 0; f < 3 * kCMax; ++f)
+                for (int f = 0; f < 3 * CM; ++f)
                     if (f < nf) gf = fma(fc[f], fr[f], gf);
             } else if (cl >= NJ + 6) {
                 const int fl = cl - NJ - 6;
 #pragma unroll
-                for (int f = 0; f < 3 * kCMax; ++f)
+                for (int f = 0; f < 3 * CM; ++f)
                     if (f == fl) gf = fc[f];
             }
             S[L.GM + ci * L.GS + cl] = fma(gf, ieps, g);
@@ -749,18 +753,18 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         // lane i's own M row and contact-Jacobian column, re-read (L2) rather than held
         const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
         const int moff = (int)(8 * ic);
-        double mr[NQ], jr[3 * kCMax]; // unconditional (clamped) loads: one round trip
+        double mr[NQ], jr[3 * CM]; // unconditional (clamped) loads: one round trip
 #pragma unroll
         for (int j = 0; j < NQ; ++j) mr[j] = bload(Mrs, moff, 8 * (j < n ? j : n - 1) * n);
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
         const int joff = (int)(8 * ic);
 #pragma unroll
-        for (int f = 0; f < 3 * kCMax; ++f)
+        for (int f = 0; f < 3 * CM; ++f)
             jr[f] = bload(Jrs, joff, 8 * (6 * (f < nf ? f / 3 : 0) + f % 3) * n);
 #pragma unroll
         for (int j = 0; j < NQ; ++j) t = fma(j < n ? mr[j] : 0.0, S[L.XV + (j < n ? j : 0)], t);
 #pragma unroll
-        for (int f = 0; f < 3 * kCMax; ++f)
+        for (int f = 0; f < 3 * CM; ++f)
             t = fma((f < nf && ((cm >> (f / 3)) & 1)) ? -jr[f] : 0.0, S[L.XV + n + (f < nf ? f : 0)], t);
         tau_i = t;
     }
