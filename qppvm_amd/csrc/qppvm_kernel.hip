@@ -426,6 +426,13 @@ template <int NP, int M0>
 constexpr bool kInlineRepair = false;
 #endif
 
+// Waves per SIMD the n > 32 fast kernel is compiled for. 2 caps it at 256 registers (it spills,
+// ~760 B of scratch per lane) but doubles the resident instances: A/B n = 39 config 1 (one box,
+// profiles/r02_v10_ab_*) 30.3 -> 35.5 M QP/s; 1 lets it use 512 VGPR + AGPR without spills.
+#ifndef WBQ_NP64_WAVES
+#define WBQ_NP64_WAVES 2
+#endif
+
 // ====================================================================== fast path
 // An instance whose equality-constrained optimum violates a bound needs the dual active
 // set: with MERGED (NP = 32, where the active-set layout fits next to the fast one) it runs
@@ -436,7 +443,7 @@ constexpr bool kInlineRepair = false;
 // wave's stage under the 63 outstanding vector loads, and the elimination carries 3
 // right-hand sides instead of 5.
 template <int NP, int M0, bool MERGED, int TM>
-__global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const QppvmArgs a)
+__global__ __launch_bounds__(64, NP == 32 ? 2 : WBQ_NP64_WAVES) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -497,7 +504,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_fast_kernel(const 
     // contiguous -- coalesced loads straight into the elimination registers.
     double A[NP];
 #pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    for (int r = 0; r < NP; ++r) // rows past n are not loaded (n is wave-uniform: a scalar branch)
+        A[r] = r < n ? bload(Mrs, moff, 8 * r * n) : 0.0;
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
