@@ -504,8 +504,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : WBQ_NP64_WAVES) void qppvm_fast_
     // contiguous -- coalesced loads straight into the elimination registers.
     double A[NP];
 #pragma unroll
-    for (int r = 0; r < NP; ++r) // rows past n are not loaded (n is wave-uniform: a scalar branch)
-        A[r] = r < n ? bload(Mrs, moff, 8 * r * n) : 0.0;
+    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
