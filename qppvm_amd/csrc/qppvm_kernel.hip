@@ -426,12 +426,12 @@ template <int NP, int M0>
 constexpr bool kInlineRepair = false;
 #endif
 
-// Waves per SIMD the n > 32 fast kernel is compiled for. 2 caps it at 256 registers (it spills,
-// ~760 B of scratch per lane) but doubles the resident instances: A/B n = 39 config 1 (one box,
-// profiles/r02_v10_ab_*) 30.3 -> 35.5 M QP/s; 1 lets it use 512 VGPR + AGPR without spills.
-#ifndef WBQ_NP64_WAVES
-#define WBQ_NP64_WAVES 2
-#endif
+// Waves per SIMD of the n > 32 fast kernel (template W). W = 2 caps it at 256 registers (it
+// spills, ~760 B of scratch per lane) but doubles the resident instances: A/B n = 39 config 1
+// (one box, profiles/r02_v10_ab_*) 30.3 -> 35.5 M QP/s. W = 1 (512 VGPR + AGPR, no spills) has
+// the shorter single-instance latency: config 0's n = 39 plugin tick 73 us vs 110 us with W = 2.
+// Batches that fit one wave round at W = 1 (<= 1,024 instances) take W = 1.
+constexpr int kNp64OneRound = 1024;
 
 // ====================================================================== fast path
 // An instance whose equality-constrained optimum violates a bound needs the dual active
@@ -442,8 +442,11 @@ constexpr bool kInlineRepair = false;
 // 12 J-row loads and 2 pose loads per lane instead of 24 and 3 (TM = 4), which keeps a
 // wave's stage under the 63 outstanding vector loads, and the elimination carries 3
 // right-hand sides instead of 5.
-template <int NP, int M0, bool MERGED, int TM>
-__global__ __launch_bounds__(64, NP == 32 ? 2 : WBQ_NP64_WAVES) void qppvm_fast_kernel(const QppvmArgs a)
+// MR: rows of M loaded (n <= MR, compile time; the rest of the NP padding rows are identity
+// without a load): with n = 39 and MR = 40 the stage issues ~59 loads per lane instead of ~83,
+// under the 63 outstanding vector memory operations.
+template <int NP, int M0, bool MERGED, int TM, int W, int MR>
+__global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : WBQ_NP64_WAVES) void qppvm_fast_
     // contiguous -- coalesced loads straight into the elimination registers.
     double A[NP];
 #pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    for (int r = 0; r < NP; ++r) A[r] = r < MR ? bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n) : 0.0;
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
     S[L.QD + i] = row ? qd_i : 0.0;
@@ -768,10 +771,20 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     const unsigned grid = (unsigned)((a.B + IPW - 1) / IPW);
     if (grid == 0) return hipSuccess;
     constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
-    hipError_t e = a.ntasks <= 2
-                       ? launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED, 2>, a, grid, stream)
-                       : launch_one<NP, FastLdsLayout<NP, MERGED>>(qppvm_fast_kernel<NP, M0, MERGED, kTMax>, a, grid,
-                                                                   stream);
+    using Lay = FastLdsLayout<NP, MERGED>;
+    hipError_t e;
+    if constexpr (NP == 32) {
+        e = a.ntasks <= 2 ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 32>, a, grid, stream)
+                          : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 2, 32>, a, grid, stream);
+    } else if (a.ntasks > 2) {
+        e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 1, 64>, a, grid, stream);
+    } else if (a.n <= 40) { // CENTAURO-sized (n = 39)
+        e = a.B > kNp64OneRound ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 40>, a, grid, stream)
+                                : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 40>, a, grid, stream);
+    } else {
+        e = a.B > kNp64OneRound ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 64>, a, grid, stream)
+                                : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 64>, a, grid, stream);
+    }
     if (e != hipSuccess) return e;
     if (mid) { // end of the dominant launch
         e = hipEventRecord(mid, stream);
