@@ -131,7 +131,7 @@ struct W1mGi {
 
 // The whole W1 = M solve of instance b by one wave. rep (the repair kernel): limits and
 // level-0 targets from the RepairIn block at R instead of tau_min/max and b0.
-template <int NQ, int M0>
+template <int NQ, int M0, int TM>
 __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b, int i, const double *R, int it0,
                                           int st0)
 {
@@ -148,14 +148,14 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     const int voff = (int)(8 * ic);
     const double q_i = bload(rsrc_at(a.q, bu, B, n), voff, 0), qd_i = bload(rsrc_at(a.qd, bu, B, n), voff, 0);
     const double qref_i = bload(rsrc_at(a.qref, bu, B, n), voff, 0), h_i0 = bload(rsrc_at(a.h, bu, B, n), voff, 0);
-    double jv[kTMax * 6];
+    double jv[TM * 6];
     {
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.J, bu, B, (long)T * 6 * n);
         const int joff = (int)(8 * ic);
 #pragma unroll
-        for (int rr = 0; rr < kTMax * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
+        for (int rr = 0; rr < TM * 6; ++rr) jv[rr] = bload(Jrs, joff, 8 * (rr < T * 6 ? rr : T * 6 - 1) * n);
     }
-    constexpr int kPoseIt = (kTMax * 24 + 63) / 64;
+    constexpr int kPoseIt = (TM * 24 + 63) / 64;
     double pv[kPoseIt];
     {
         const __amdgpu_buffer_rsrc_t Prs = rsrc_at(a.pose, bu, B, (long)T * 12);
@@ -182,7 +182,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     S[L.QD + i] = row ? qd_i : 0.0;
     if (i < NQ) {
 #pragma unroll
-        for (int rr = 0; rr < kTMax * 6; ++rr)
+        for (int rr = 0; rr < TM * 6; ++rr)
             if (rr < T * 6) S[L.JR + rr * NQ + i] = row ? jv[rr] : 0.0;
     }
 #pragma unroll
@@ -222,7 +222,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     __syncthreads();
     if (i < NQ) { // J_t^T F_t (joint i)
 #pragma unroll
-        for (int t = 0; t < kTMax; ++t) {
+        for (int t = 0; t < TM; ++t) {
             double c = 0.0;
             if (t < T)
 #pragma unroll
@@ -406,16 +406,16 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     }
 }
 
-template <int NQ, int M0>
+template <int NQ, int M0, int TM>
 __global__ __launch_bounds__(64) void qppvm_w1m_kernel(const QppvmArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    w1m_solve<NQ, M0>(a, smem, blockIdx.x, threadIdx.x, nullptr, 0, 0);
+    w1m_solve<NQ, M0, TM>(a, smem, blockIdx.x, threadIdx.x, nullptr, 0, 0);
 }
 
 // Level-0 repair for W1 = M: BVLS for y* and the pinned limits (level0_repair of the W1 = I
 // path, one instance per wave), then the W1 = M solve again with those.
-template <int NQ, int M0>
+template <int NQ, int M0, int TM>
 __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -467,19 +467,19 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
             R[RepairIn::YS + i] = y;
         }
         __syncthreads();
-        w1m_solve<NQ, M0>(a, smem, b, i, R, ro.it, ro.status);
+        w1m_solve<NQ, M0, TM>(a, smem, b, i, R, ro.it, ro.status);
     }
 }
 
-template <int NQ, int M0>
+template <int NQ, int M0, int TM>
 hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     const W1mLayout L(a.n, a.ntasks, a.m0, NQ, 1 + M0);
     if (L.ME > 64) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
-    hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0>, lds);
+    hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0, TM>, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((qppvm_w1m_kernel<NQ, M0>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((qppvm_w1m_kernel<NQ, M0, TM>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (mid) {
@@ -488,10 +488,10 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     const int ws = ActiveLayout<64>(a.ntasks, a.m0).SIZE;
     const size_t lds2 = sizeof(double) * ((ws > L.SIZE ? ws : L.SIZE) + RepairIn::SIZE);
-    e = ensure_dynamic_lds((const void *)qppvm_w1m_repair_kernel<NQ, M0>, lds2);
+    e = ensure_dynamic_lds((const void *)qppvm_w1m_repair_kernel<NQ, M0, TM>, lds2);
     if (e != hipSuccess) return e;
     const unsigned grid = a.B < (int)kFollowGrid ? (unsigned)a.B : kFollowGrid;
-    hipLaunchKernelGGL((qppvm_w1m_repair_kernel<NQ, M0>), dim3(grid), dim3(64), lds2, stream, a);
+    hipLaunchKernelGGL((qppvm_w1m_repair_kernel<NQ, M0, TM>), dim3(grid), dim3(64), lds2, stream, a);
     return hipGetLastError();
 }
 
@@ -500,8 +500,16 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     if (a.B <= 0) return hipSuccess;
-    if (a.n <= 32) return a.m0 <= 6 ? launch_w1m_t<32, 6>(a, stream, mid) : launch_w1m_t<32, kM0Max>(a, stream, mid);
-    return a.m0 <= 6 ? launch_w1m_t<64, 6>(a, stream, mid) : launch_w1m_t<64, kM0Max>(a, stream, mid);
+    // TM = 2 when at most two tasks: 12 J-row loads per lane instead of 24 (the stage stays under
+    // the 63 outstanding vector loads, as the W1 = I fast kernel)
+    if (a.ntasks <= 2) {
+        if (a.n <= 32)
+            return a.m0 <= 6 ? launch_w1m_t<32, 6, 2>(a, stream, mid) : launch_w1m_t<32, kM0Max, 2>(a, stream, mid);
+        return a.m0 <= 6 ? launch_w1m_t<64, 6, 2>(a, stream, mid) : launch_w1m_t<64, kM0Max, 2>(a, stream, mid);
+    }
+    if (a.n <= 32)
+        return a.m0 <= 6 ? launch_w1m_t<32, 6, kTMax>(a, stream, mid) : launch_w1m_t<32, kM0Max, kTMax>(a, stream, mid);
+    return a.m0 <= 6 ? launch_w1m_t<64, 6, kTMax>(a, stream, mid) : launch_w1m_t<64, kM0Max, kTMax>(a, stream, mid);
 }
 
 }  // namespace wbq
