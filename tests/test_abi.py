@@ -110,3 +110,53 @@ def test_w1m_capacity_rejected_before_device(lib):
     assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_UNSUPPORTED
     d.joint_weight = 2
     assert lib.wbq_create(ctypes.byref(d), 0, ctypes.byref(h)) == wbq.E_INVALID
+
+
+def test_rbd_model_validated_before_device(lib):
+    """wbq_rbd_create rejects a model that is not a topologically ordered tree of unit joint
+    axes, or task links outside it, before any device call (CPU)."""
+    import numpy as np
+    from qppvm_amd.rbd import _Desc, centauro_like
+
+    m = centauro_like()
+
+    def create(parent=None, axis=None, task_link=None, n=None):
+        keep = {k: np.ascontiguousarray(getattr(m, k), dtype=np.int32 if k in ("parent", "task_link") else np.float64)
+                for k in ("parent", "X_fixed", "axis", "mass", "com", "inertia", "task_link")}
+        if parent is not None:
+            keep["parent"] = np.ascontiguousarray(parent, dtype=np.int32)
+        if axis is not None:
+            keep["axis"] = np.ascontiguousarray(axis, dtype=np.float64)
+        if task_link is not None:
+            keep["task_link"] = np.ascontiguousarray(task_link, dtype=np.int32)
+        d = _Desc()
+        d.n = m.n if n is None else n
+        for k, v in keep.items():
+            setattr(d, k, v.ctypes.data)
+        d.ntasks, d.max_batch = len(keep["task_link"]), 4
+        h = ctypes.c_void_p()
+        return lib.wbq_rbd_create(ctypes.byref(d), 0, ctypes.byref(h))
+
+    bad_parent = m.parent.copy()
+    bad_parent[3] = 5  # a parent after its child
+    assert create(parent=bad_parent) == wbq.E_INVALID
+    bad_axis = m.axis.copy()
+    bad_axis[2] *= 2.0  # not unit
+    assert create(axis=bad_axis) == wbq.E_INVALID
+    assert create(task_link=[m.n]) == wbq.E_INVALID
+    assert create(n=65) == wbq.E_INVALID
+
+
+def test_plant_states_are_euler_stable():
+    """Config 4's plant-scaled synthetic states keep dt * Dc * lambda_max(G M^-1 G^T) below 2 at
+    the reference gains, the SURVEY distribution does not (bench.py euler_stability)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from qppvm_amd.problem import QPPVMProblem
+    from qppvm_amd.synth import qppvm_instances
+    prob = QPPVMProblem(n=30)
+    plant = bench.euler_stability(prob, qppvm_instances(prob, 64, seed=1, plant=True), 1e-3)
+    survey = bench.euler_stability(prob, qppvm_instances(prob, 64, seed=1), 1e-3)
+    assert plant["max"] < 2.0 < survey["median"]
