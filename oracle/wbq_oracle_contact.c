@@ -187,6 +187,18 @@ int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const doubl
                 if (kind[a] >= 0 && r[a] > 1e-12 * cmaxd(rmax, 1e-300) && lam[a] / r[a] < t1) t1 = lam[a] / r[a], blk = a;
             const double t2 = (zz > 1e-14 * nn) ? -sp / zz : INFINITY;
             if (!isfinite(t1) && !isfinite(t2)) {
+                /* p depends on the active normals and nothing can be dropped. A violation at the
+                 * roundoff of the rows it depends on (a degenerate face: the level-1 problem after a
+                 * level-0 repair holds the waist rows at y0*, which the active bounds already imply)
+                 * is not an inconsistency: p is met as far as the data determine it, so it is
+                 * skipped for this pass. A first step only: once partial steps moved x for p its
+                 * multiplier is in play and the rows are genuinely inconsistent. */
+                double ps = 0.0;
+                for (int i = 0; i < n; ++i) ps += fabs(np[i] * x[i]);
+                if (lamp == 0.0 && -sp <= 1e-9 * (1.0 + fabs(bp) + ps)) {
+                    if (pk >= 0) onrow[pk] = 2; /* skipped: no multiplier, not re-selected */
+                    break;
+                }
                 status = WBQ_REF_INFEASIBLE;
                 goto out;
             }
@@ -372,7 +384,10 @@ int wbq_ref_contact_one(const wbq_ref_contact_desc *d, const wbq_ref_contact_ins
     if (l0_repaired) *l0_repaired = 0;
     /* level 0 attained at b_w (the generic case): level 1 with J_w qdd = b_w */
     status = wbq_ref_dual_qp(nx, L.H, L.g, L.me, L.E, L.e, L.mi, L.C, L.clo, L.chi, x, &it1);
-    if (status == WBQ_REF_INFEASIBLE) {
+    /* an unattainable waist target shows as "no step" (infeasible), but near the degenerate face it
+     * can also end the active set numerically (status 3) or cycling (1): every failure tries level 0
+     * first (the GPU routes the same statuses to its repair kernel, contact_kernel.hip) */
+    if (status != WBQ_REF_OK) {
         /* level 0 not attainable at b_w: y0* from the level-0 QP (its Hessian J_w^T J_w is
          * singular; a relative 1e-10 ridge only picks among level-0 optima), then level 1 */
         level_qp Z;

@@ -106,7 +106,10 @@ struct ContactLayout {
             HR = TT;                  // (unused: NQ == 64 && tr only)
         }
         // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns
-        const int tt = tr ? NX * TS : 12 * TS; // (!tr: scratch for the T_E rows)
+        // (!tr: scratch for the T_E rows and for dual_gi's re-factorisation, KMR rows of KMR + 1;
+        // KMR = the register slot capacity of launch_nq)
+        const int kmr = nc <= 2 ? 18 : 24;
+        const int tt = tr ? NX * TS : (12 * TS > kmr * (kmr + 1) ? 12 * TS : kmr * (kmr + 1));
         o += tt > ov ? tt : ov;
         XV = o; o += 64;          // x
         X0 = o; o += 64;          // x0 = -H^-1 g
@@ -723,7 +726,8 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
             for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
         }
-        dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
+        dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, SREG ? KMR + 1 : L.TS}, i, Trow, Tcol, GA, kind,
+                    lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }
     if (gs.status != 1 && gs.status != 3) break;
@@ -732,8 +736,11 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     const int iters = gs.iters + it0;
     if constexpr (!REPAIR) {
         // no step exists: the waist task is not attainable at b_w (the rows are boxes in
-        // (tau_a, f), so nothing else can be infeasible) -- the repair kernel solves level 0 first
-        if (status == 2 && !a.limits_crossed && a.wl) {
+        // (tau_a, f), so nothing else can be infeasible) -- the repair kernel solves level 0 first.
+        // A loop that ends at the step or rounds cap (1) or on a numerically dependent set (3) goes
+        // there too: an unattainable waist target often shows as cycling among nearly dependent rows
+        // rather than as a clean "no step", and the repair's pinned level 1 is the robust route
+        if ((status == 2 || status == 1 || (status == 3 && !notspd)) && !a.limits_crossed && a.wl) {
             if (i == 0) {
                 a.status[b] = -2;
                 const int idx = atomicAdd(&a.work[a.epoch * 2 + 1], 1);

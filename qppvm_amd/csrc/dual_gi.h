@@ -67,6 +67,17 @@ struct SlotVec<KM, true> {
             v[j] = (cond && j < cnt) ? w : v[j];
         }
     }
+    // after refactor_T: row `row` (this lane's slot row) of T from the LDS factor, or column
+    // `row` (col = true); zero past cnt
+    __device__ void load_factor(const double *tb, int ts, int row, int cnt, bool col)
+    {
+        const bool own = row < cnt;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double w = tb[col ? j * ts + (own ? row : 0) : (own ? row : 0) * ts + j];
+            v[j] = (own && j < cnt && (col ? j >= row : j <= row)) ? w : 0.0;
+        }
+    }
     __device__ void shift_down(int c, int cnt) // v[j] = v[j + 1] for c <= j < cnt - 1
     {
 #pragma unroll
@@ -116,6 +127,7 @@ struct SlotVec<KM, false> {
         if (cond)
             for (int j = 0; j < cnt; ++j) p[j] = src[j];
     }
+    __device__ void load_factor(const double *, int, int, int, bool) {} // the factor is these rows
     __device__ void shift_down(int c, int cnt)
     {
         for (int j = c; j + 1 < cnt; ++j) p[j] = p[j + 1];
@@ -161,6 +173,7 @@ struct TColView {
     __device__ void zero_from(int) {}
     __device__ void put(int, bool, double) {}
     __device__ void put_dyn(int, bool, double) {}
+    __device__ void load_factor(const double *, int, int, int, bool) {}
     __device__ double dot(const double *b, int cnt) const
     {
         double s = 0.0;
@@ -213,9 +226,11 @@ constexpr int kGiRounds = 8; // x rebuilds (each followed by a re-check of every
 constexpr int kGiPasses = 5; // per rebuild: x from the multipliers, then up to 4 refinement passes
 constexpr double kDropPivot = 1e-9; // relative pivot below which a slot is dropped when a rebuild misses
 
-// LDS scratch vectors of the loop (72 doubles each: slot dots read 8 past the active count)
+// LDS scratch vectors of the loop (72 doubles each: slot dots read 8 past the active count), and
+// where the rebuild re-factors T: rows TB + r * TST (the T rows themselves when they live in LDS,
+// else scratch of at least KM rows of KM + 1)
 struct GiVecs {
-    int VV, LV, RV, WV, AC;
+    int VV, LV, RV, WV, AC, TB, TST;
 };
 
 // Lane state. Slot a (lane a < k) = the a-th active row: act (its index), sgn (normal =
@@ -226,6 +241,58 @@ struct GiState {
     double sgn = 1.0, lam = 0.0;
     bool aeq = false, onact = false;
 };
+
+// T = L^-1 of the active-set Gram Gamma_AA (signed normals, slot order) from scratch, into LDS rows
+// S[tb + r ts]: a left-looking Cholesky (lane r computes row r of L; one barrier per column), then
+// the triangle inverted in place column by column from the last (T[r][c] = -sum_{q>c} T[r][q]
+// L[q][c] / L[c][c]). The incremental factor the loop carries (closed-form appends, re-appends after
+// a drop) picks up the roundoff of every cancellation d^2 = Gamma_pp - |l|^2; on a nearly dependent
+// active set (relative pivots ~1e-11, scripts/emulate_dual_gi.py) it is too poor for the refinement
+// of (x, lambda) to converge, the rebuilt x misses an active row, and the slot-drop / re-add cycle
+// ends at the rounds cap. A backward-stable factor of the final set is what the refinement needs.
+template <class P>
+__device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k, const GiState &g)
+{
+    const bool own = i < k;
+#pragma unroll 1
+    for (int c = 0; c < k; ++c) {
+        const int ac = __shfl(g.act, c);
+        const double sc = __shfl(g.sgn, c);
+        if (own) S[tb + i * ts + c] = c <= i ? g.sgn * sc * pb.gamma(g.act, ac) : 0.0;
+    }
+    __syncthreads();
+    const double *ri = S + tb + (own ? i : 0) * ts;
+#pragma unroll 1
+    for (int c = 0; c < k; ++c) {
+        const double *rc = S + tb + c * ts;
+        double s = 0.0;
+        if (own && i >= c) {
+            double s0 = ri[c], s1 = 0.0;
+            int j = 0;
+            for (; j + 1 < c; j += 2) {
+                s0 = fma(-ri[j], rc[j], s0);
+                s1 = fma(-ri[j + 1], rc[j + 1], s1);
+            }
+            if (j < c) s0 = fma(-ri[j], rc[j], s0);
+            s = s0 + s1;
+        }
+        const double gcc = pb.gamma(__shfl(g.act, c), __shfl(g.act, c));
+        const double d = fmax(bcast(s, c), 1e-30 * gcc); // a non-positive pivot: the miss check drops it
+        const double il = frsq(d);
+        if (own && i >= c) S[tb + i * ts + c] = i == c ? d * il : s * il;
+        __syncthreads();
+    }
+#pragma unroll 1
+    for (int c = k - 1; c >= 0; --c) {
+        const double lcc = S[tb + c * ts + c];
+        double acc = 0.0;
+        if (own && i > c)
+            for (int q = c + 1; q <= i; ++q) acc = fma(ri[q], S[tb + q * ts + c], acc);
+        __syncthreads();
+        if (own && i >= c) S[tb + i * ts + c] = i == c ? 1.0 / lcc : -acc / lcc;
+        __syncthreads();
+    }
+}
 
 // The loop itself (lane i = constraint row i; kind 0 disabled, 1 equality already in the
 // active set, 2 a row with limits [lo, hi], lo == hi an equality added when violated).
@@ -305,6 +372,11 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 }
                 ++g.rounds;
                 dirty = false;
+                if (g.k > 0) { // a backward-stable factor of the final set for the refinement
+                    refactor_T(pb, S, V.TB, V.TST, i, g.k, g);
+                    Trow.load_factor(S + V.TB, V.TST, i, g.k, false);
+                    Tcol.load_factor(S + V.TB, V.TST, i, g.k, true);
+                }
                 const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act); // all lanes active
                 S[V.RV + i] = i < g.k ? g.sgn * g.lam : 0.0;
                 S[V.AC + i] = (double)g.act;

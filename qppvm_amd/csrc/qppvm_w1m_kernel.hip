@@ -365,7 +365,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     }
     {
         const W1mGi pb{S, &L, m0, n, i, n};
-        dual_gi<64>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
+        dual_gi<64>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
                     a.max_iter);
     }
     __syncthreads();

@@ -11,6 +11,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import kkt  # noqa: E402
 import oracle  # noqa: E402
 from qppvm_amd import wbq  # noqa: E402
 from qppvm_amd.problem import ContactProblem  # noqa: E402
@@ -22,7 +24,7 @@ q = float(args[1]) if len(args) > 1 else 0.4
 seed0 = int(args[2]) if len(args) > 2 else 100
 seeds = int(args[3]) if len(args) > 3 else 20
 MASKS4 = [0b0011, 0b0111, 0b1111, 0b0101, 0b1010, 0b1100]
-tot = dict(solved=0, repaired=0, miss=0, miss_rep=0, wrong_st0=0, gpu_only=0)
+tot = dict(solved=0, repaired=0, miss=0, miss_rep=0, wrong_st0=0, gpu_only=0, gpu_only_cert_bad=0)
 for seed in range(seed0, seed0 + seeds):
     free = ContactProblem(n=n, nc=4)
     inp = contact_instances(free, 64, seed=seed, masks=MASKS4)
@@ -31,6 +33,7 @@ for seed in range(seed0, seed0 + seeds):
     tau_r, x_r, st_r, it_r, rep = oracle.contact_batch(prob, inp)
     s = wbq.ContactSolver(prob, max_batch=64)
     tau, st, it = s.solve_batch(inp)
+    xgpu = s.x()
     s.close()
     e = np.abs(tau - tau_r).max(axis=1) / np.maximum(1.0, np.abs(tau_r).max(axis=1))
     solved = st_r == 0
@@ -41,6 +44,14 @@ for seed in range(seed0, seed0 + seeds):
     tot["miss_rep"] += int((miss & (rep != 0)).sum())
     tot["gpu_only"] += int((~solved & (st == 0)).sum())
     tot["wrong_st0"] += int((miss & (st == 0)).sum())  # a wrong tau reported as solved
+    # instances only the GPU solves: KAT-4 certificates of level 0 and level 1 (tests/kkt.py)
+    for b in np.where(~solved & (st == 0))[0]:
+        x = xgpu[b]
+        l0, y = kkt.contact_level0_certificate(oracle, prob, inp, b, x)
+        c = kkt.contact_certificate(oracle, prob, inp, b, x, waist=y)
+        if l0 > 1e-9 or c["primal"] > 1e-9 or c["stat"] > 1e-9 or c["sign"] > 1e-9:
+            tot["gpu_only_cert_bad"] += 1
+            print(f"  b={b}: GPU-only solution fails its certificate: level0 {l0:.2e} {c}")
     print(f"seed {seed}: oracle solves {int(solved.sum())} (repaired {int((solved & (rep != 0)).sum())}), "
           f"GPU misses {int(miss.sum())} {[(int(b), int(st[b])) for b in np.where(miss)[0]]}, "
           f"GPU solves where the oracle fails "

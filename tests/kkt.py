@@ -112,7 +112,9 @@ def contact_certificate(oracle, prob, inp, b, x, waist=None):
     cx = C @ x
     scale = 1.0 + max(np.abs(e).max(), np.abs(np.concatenate([clo, chi])[np.isfinite(np.concatenate([clo, chi]))]).max(initial=0.0))
     primal = max(np.abs(E @ x - e).max(), max(0.0, (clo - cx).max(initial=0.0), (cx - chi).max(initial=0.0))) / scale
-    at_lo, at_hi = _active(cx, clo, chi, 1e-9)
+    # a row met to 1e-8 relative is active: the dual loop accepts its active rows at that level
+    # (qppvm_amd/csrc/dual_gi.h, the final re-check)
+    at_lo, at_hi = _active(cx, clo, chi, 1e-8)
     act = np.where(at_lo | at_hi)[0]
     K = np.concatenate([E.T, C[act].T], axis=1)
     r = H @ x + g

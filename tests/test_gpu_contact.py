@@ -87,34 +87,44 @@ def test_contact_torque_rows(wbq_mod, oracle_lib, n, q, nc):
     assert np.all(np.abs(tau[:, 6:]) <= lim)
 
 
-@pytest.mark.parametrize("seed", [101, 108, 119])
-def test_contact_level0_repair(wbq_mod, oracle_lib, seed):
+# the one instance of the sweep below the GPU does not solve (seed 105, b = 62: the repair's dual
+# loop ends at the step cap on a nearly singular vertex)
+MAX_MISS = 1
+
+
+def test_contact_level0_repair(wbq_mod, oracle_lib):
     """Level 0 not attainable (ForceAcc.cpp:131-137,189: the waist task at b_w is out of reach of
     the torque and force boxes -- 6 actuated joints, limits at the 40 % quantile): the GPU solves
     level 0 first (contact_kernel.hip:contact_level0, BVLS) and level 1 keeps the waist at y0*.
-    Every instance the oracle solves -- repaired or not -- matches it (status and tau); where the
-    oracle itself fails numerically (status 2 or 3 in this degenerate regime), a GPU solution must
-    carry the level-0 and level-1 KKT certificates (tests/kkt.py). This regime is degenerate by
-    construction (the level-0 face makes the final active sets nearly singular); over 20 seeds
-    (scripts/diag_contact_repair.py) the GPU matches 98.4 % of the instances the
-    oracle solves and returns a failure status on the others; these three seeds match completely."""
+    The whole 20-seed sweep (1,280 instances, scripts/diag_contact_repair.py): every instance the
+    oracle solves -- repaired or not -- matches it (status and tau), except at most MAX_MISS that
+    end with a failure status (tau = h, never a wrong tau reported as solved); where the oracle
+    itself fails, a GPU solution must carry the level-0 and level-1 KKT certificates (tests/kkt.py).
+    This regime is degenerate by construction (the level-0 face makes the final active sets
+    nearly singular)."""
     import kkt
     n, nc = 12, 4
-    free = ContactProblem(n=n, nc=nc)
-    inp = contact_instances(free, 64, seed=seed, masks=MASKS4)
-    tau_free = oracle_lib.contact_batch(free, inp)[0]
-    prob = ContactProblem(n=n, nc=nc, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), 0.4)))
-    tau_r, x_r, st_r, _, rep = oracle_lib.contact_batch(prob, inp)
-    tau, x, st, it = gpu_solve(wbq_mod, prob, inp)
-    solved = st_r == 0
-    assert (solved & (rep != 0)).sum() >= 4  # the repair path really runs
-    np.testing.assert_array_equal(st[solved], 0)
-    assert rel_err(tau[solved], tau_r[solved]) <= TOL, rel_err(tau[solved], tau_r[solved])
-    np.testing.assert_array_equal(tau[st != 0], inp["h"][st != 0])
-    for b in np.where(~solved & (st == 0))[0]:
-        l0, y = kkt.contact_level0_certificate(oracle_lib, prob, inp, b, x[b])
-        c = kkt.contact_certificate(oracle_lib, prob, inp, b, x[b], waist=y)
-        assert l0 <= 1e-9 and max(c["primal"], c["stat"], c["sign"]) <= 1e-9, (b, l0, c)
+    tot = dict(solved=0, repaired=0, miss=0)
+    for seed in range(100, 120):
+        free = ContactProblem(n=n, nc=nc)
+        inp = contact_instances(free, 64, seed=seed, masks=MASKS4)
+        tau_free = oracle_lib.contact_batch(free, inp)[0]
+        prob = ContactProblem(n=n, nc=nc, torque_rows=True, tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), 0.4)))
+        tau_r, x_r, st_r, _, rep = oracle_lib.contact_batch(prob, inp)
+        tau, x, st, it = gpu_solve(wbq_mod, prob, inp)
+        solved = st_r == 0
+        tot["solved"] += int(solved.sum())
+        tot["repaired"] += int((solved & (rep != 0)).sum())
+        ok = solved & (st == 0)
+        assert rel_err(tau[ok], tau_r[ok]) <= TOL, (seed, rel_err(tau[ok], tau_r[ok]))
+        tot["miss"] += int((solved & (st != 0)).sum())
+        np.testing.assert_array_equal(tau[st != 0], inp["h"][st != 0])
+        for b in np.where(~solved & (st == 0))[0]:
+            l0, y = kkt.contact_level0_certificate(oracle_lib, prob, inp, b, x[b])
+            c = kkt.contact_certificate(oracle_lib, prob, inp, b, x[b], waist=y)
+            assert l0 <= 1e-9 and max(c["primal"], c["stat"], c["sign"]) <= 1e-9, (seed, b, l0, c)
+    assert tot["repaired"] >= 100, tot  # the repair path really runs
+    assert tot["miss"] <= MAX_MISS, tot
 
 
 def test_contact_structure_and_edges(wbq_mod):
