@@ -249,7 +249,9 @@ struct GiState {
 // a drop) picks up the roundoff of every cancellation d^2 = Gamma_pp - |l|^2; on a nearly dependent
 // active set (relative pivots ~1e-11, scripts/emulate_dual_gi.py) it is too poor for the refinement
 // of (x, lambda) to converge, the rebuilt x misses an active row, and the slot-drop / re-add cycle
-// ends at the rounds cap. A backward-stable factor of the final set is what the refinement needs.
+// ends at the rounds cap. A backward-stable factor of the final set is what the refinement needs;
+// the loop re-factors only after a rebuild on the incremental factor missed an active row (the
+// common path keeps its cost: configs 1 and 2 of the contact form rebuild once, cleanly).
 template <class P>
 __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k, const GiState &g)
 {
@@ -304,6 +306,7 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                                         int maxit)
 {
     bool need_select = true, dirty = true, recheck = false;
+    bool refac = false; // the next rebuild re-factors T first (after one that missed an active row)
     int cp = 0;
     double sgp = 1.0, bnd = 0.0, lamp = 0.0;
     bool peq = false;
@@ -372,11 +375,13 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 }
                 ++g.rounds;
                 dirty = false;
-                if (g.k > 0) { // a backward-stable factor of the final set for the refinement
+                if (refac && g.k > 0) { // a backward-stable factor of the final set for the refinement
                     refactor_T(pb, S, V.TB, V.TST, i, g.k, g);
                     Trow.load_factor(S + V.TB, V.TST, i, g.k, false);
                     Tcol.load_factor(S + V.TB, V.TST, i, g.k, true);
                 }
+                const bool fresh = refac;
+                refac = false;
                 const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act); // all lanes active
                 S[V.RV + i] = i < g.k ? g.sgn * g.lam : 0.0;
                 S[V.AC + i] = (double)g.act;
@@ -414,6 +419,10 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 // of a nearly dependent active set) is garbage and so is x: fail loudly
                 const double miss = (kind != 0 && g.onact) ? fmin(fabs(s_i - lo), fabs(s_i - hi)) / (1.0 + fabs(s_i)) : 0.0;
                 if (imax<64>(miss) > 1e-8) {
+                    if (!fresh) { // the incremental factor first: rebuild once more on a fresh one
+                        refac = dirty = recheck = true;
+                        continue;
+                    }
                     // a nearly dependent row added by the loop: drop the slot with the smallest
                     // relative pivot d^2 / Gamma_pp = 1 / (T_aa^2 Gamma_pp) -- an implied row, which
                     // the exact activities of the next rebuild still meet -- and rebuild; the

@@ -57,8 +57,10 @@ private:
     int _solver_errors = 0;
     int _cmask = 0xF;
 
-    Eigen::VectorXd _k, _d, _q, _qdot, _q_ref, _tau, _x, _qddot_value, _h;
-    Eigen::VectorXd _initial_com;
+    Eigen::VectorXd _k, _d, _q, _qdot, _q_ref, _tau, _tau_c, _x, _qddot_value, _h;
+    Eigen::Vector3d _initial_com; // ForceAcc.h:69 (the pelvis origin, ForceAcc.cpp:164)
+    Eigen::MatrixXd _Mtmp, _Jtmp;
+    std::vector<Eigen::VectorXd> _wrench_value; // [f_c; 0] per contact (ForceAcc.cpp:61,199)
     Eigen::Affine3d _waist_ref;
     std::vector<Eigen::Affine3d> _feet_ref;
     std::vector<std::string> _contact_links{"foot_fl", "foot_fr", "foot_hr", "foot_hl"}; // ForceAcc.cpp:58

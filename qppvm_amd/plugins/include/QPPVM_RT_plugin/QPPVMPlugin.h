@@ -37,13 +37,16 @@ public:
     // the dummy driver sets them before init_control_plugin / on_start
     void set_log_prefix(const std::string &prefix) { _log_prefix = prefix; }
     void set_reference_trajectory(bool on) { _set_ref = on; }
-    const Eigen::Affine3d &ee_reference(int t) const { return _ref[t]; }
+    // the Cartesian references the tasks track (t = 0 right, 1 left): the on_start poses, the
+    // left one replaced by the _set_ref sinusoid
+    const Eigen::Affine3d &ee_reference(int t) const { return _ee_ref[t]; }
 
 private:
     void sense();
     void syncFromMotorSide(XBot::RobotInterface::Ptr robot, XBot::ModelInterface::Ptr model);
-    void QPPVMControl(double time);
+    void QPPVMControl(const double time);
 
+    XBot::JointIdMap _jidmap;
     XBot::RobotInterface::Ptr _robot;
     XBot::ModelInterface::Ptr _model;
     wbq_ctx *_ctx = nullptr;
@@ -55,16 +58,19 @@ private:
     int _iters = 0;
     int _solver_errors = 0;
 
-    Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h;
+    Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h, _tau_qp;
     Eigen::VectorXd _tau_max_const, _tau_min_const;
-    Eigen::Affine3d _ref[2];
-    // _set_ref: left end-effector reference on a circle in the y-z plane (:217-223)
+    Eigen::Affine3d _ee_ref[2];
+    // _set_ref: left end-effector reference on a circle in the y-z plane (:217-223), on the
+    // reference's KDL frames (QPPVMPlugin.h:98-99)
     bool _set_ref = false;
-    Eigen::Affine3d _start_pose;
+    KDL::Frame _start_pose;
+    KDL::Frame _ref;
     std::string _log_prefix = "/tmp/qppvm_log";
     XBot::MatLogger::Ptr _matlogger;
     // per-tick input staging (instance-major, row-major: the wbq layout)
     std::vector<double> _M, _J, _pose, _pose_ref;
+    Eigen::MatrixXd _Mtmp, _Jtmp;
 };
 
 }  // namespace demo

@@ -1,6 +1,7 @@
 // ForceAcc.cpp -- XBotPlugin::ForceAccExample over libwbq. Mirrors the reference's control
-// flow (src/ForceAcc.cpp), with the OpenSoT/qpOASES solve and the inverse-dynamics
-// post-step replaced by one wbq_solve of the contact form.
+// flow (src/ForceAcc.cpp) with its own XBotInterface / Eigen spellings; the OpenSoT stack, the
+// qpOASES solve and the inverse-dynamics post-step are replaced by one wbq_solve of the contact
+// form.
 #include <ForceAccPlugin/ForceAcc.h>
 
 #include <cstdio>
@@ -8,7 +9,8 @@
 
 #include "abi_copy.h"
 
-REGISTER_XBOT_PLUGIN(ForceAccExample, XBotPlugin::ForceAccExample)
+/* Specify that the class XBotPlugin::ForceAccExample is a XBot RT plugin (ForceAcc.cpp:26) */
+REGISTER_XBOT_PLUGIN_(XBotPlugin::ForceAccExample)
 
 using namespace XBotPlugin;
 
@@ -21,23 +23,27 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
 {
     _robot = handle->getRobotInterface();
     _logger = XBot::MatLogger::getLogger(_log_prefix); // :34
-    _logger->reserve(10000);                           // _model->initLog(_logger, 10000) (:50)
+
     _robot->getStiffness(_k); // :36-39: impedance / 16, damping / 4
     _robot->getDamping(_d);
-    for (size_t j = 0; j < _k.size(); ++j) {
-        _k[j] /= 16.0;
-        _d[j] /= 4.0;
-    }
-    _model = handle->getModel(); // reference: getModel(handle->getPathToConfigFile()) :43
-    const int n = _model->getJointNum();
-    Eigen::VectorXd qhome;
-    _model->getRobotState("home", qhome); // :45-48
+    _k /= 16;
+    _d /= 4;
+
+    _model = XBot::ModelInterface::getModel(handle->getPathToConfigFile()); // :43
+    if (!_model) return false;
+
+    Eigen::VectorXd qhome; // :45-48
+    _model->getRobotState("home", qhome);
     _model->setJointPosition(qhome);
     _model->update();
+
+    _model->initLog(_logger, 10000); // :50
 
     // stack wiring (:58-137): x = [qddot; f_c x 4], wrench bounds (-1000,-1000,10)..(1000,..),
     // waist / (postural + feet) << dyn_feas << wrench bounds; the acceleration-task gains are
     // OpenSoT defaults upstream, here the build's named defaults (critically damped, Kp = 1)
+    const int n = _model->getJointNum();
+    _wrench_value.assign(_contact_links.size(), Eigen::VectorXd::Zero(6)); // :61
     wbq_contact_desc d{};
     d.n = n;
     d.n_fb = 6;
@@ -64,34 +70,45 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
     _feet_ref.resize(nc);
     _x.setZero(n + 3 * nc);
     _tau.setZero(n);
+    _tau_c.setZero(n);
     _qddot_value.setZero(n);
+    // the plugin's log (:200, :233-236): variables created here, outside the RT loop
+    for (const auto &cl : _contact_links) _logger->createVectorVariable(cl + "_wrench", 6, 1, 10000);
+    _logger->createVectorVariable("tau", n, 1, 10000);
+    _logger->createVectorVariable("tau_c", n, 1, 10000);
+    _logger->createVectorVariable("qddot_value", n, 1, 10000);
+    _logger->createVectorVariable("x", n + 3 * (int)nc, 1, 10000);
     return true;
 }
 
-void ForceAccExample::on_start(double time) // :150-165
+void ForceAccExample::on_start(double time) // :143-165
 {
     _start_time = time;
     sync_model();
     _model->getJointPosition(_q);
     _q_ref = _q; // postural reference: the start posture
-    for (size_t c = 0; c < _contact_links.size(); ++c) _model->getPose(_contact_links[c], _feet_ref[c]); // resetReference
+    // resetReference of the feet and waist tasks (:157-162): the current poses
+    for (size_t c = 0; c < _contact_links.size(); ++c) _model->getPose(_contact_links[c], _feet_ref[c]);
     _model->getPose(_waist_link, _waist_ref);
-    _model->getPointPosition(_waist_link, _initial_com); // :164 ("com" is the pelvis origin)
+    _model->getPointPosition(_waist_link, Eigen::Vector3d::Zero(), _initial_com); // :164
 }
 
-void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-253
+void ForceAccExample::control_loop(double time, double period) // :167-253
 {
-    sync_model();
+    (void)period;
+    sync_model(); // :172-178
     const int n = _model->getJointNum();
     const size_t nc = _contact_links.size();
-    // waist reference: p_init - 0.1 z, orientation as at start (:181)
-    for (int k = 0; k < 3; ++k) _waist_ref.m[4 * k + 3] = _initial_com[k] - (k == 2 ? 0.1 : 0.0);
 
-    Eigen::MatrixXd M, J;
-    Eigen::VectorXd v;
+    /* Set reference (:181): the pelvis 10 cm below its start position, orientation as at start */
+    _waist_ref.translation() = _initial_com - 0.1 * Eigen::Vector3d::UnitZ();
+
+    /* Update stack (:184): the model quantities the tasks and constraints pull, element-wise into
+     * the ABI's row-major layout (Eigen's MatrixXd is column-major) */
+    Eigen::Vector6d jdqd;
     Eigen::Affine3d P;
-    _model->getInertiaMatrix(M);
-    copy_row_major(M, n, n, _in[0].data()); // element-wise: Eigen's MatrixXd is column-major
+    _model->getInertiaMatrix(_Mtmp);
+    copy_row_major(_Mtmp, n, n, _in[0].data());
     _model->computeNonlinearTerm(_h);
     std::memcpy(_in[1].data(), _h.data(), sizeof(double) * n);
     _model->getJointPosition(_q);
@@ -99,21 +116,21 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     std::memcpy(_in[2].data(), _q.data(), sizeof(double) * n);
     std::memcpy(_in[3].data(), _qdot.data(), sizeof(double) * n);
     std::memcpy(_in[4].data(), _q_ref.data(), sizeof(double) * n);
-    _model->getJacobian(_waist_link, J);
-    copy_row_major(J, 6, n, _in[5].data());
-    _model->computeJdotQdot(_waist_link, v);
-    std::memcpy(_in[6].data(), v.data(), sizeof(double) * 6);
+    _model->getJacobian(_waist_link, _Jtmp);
+    copy_row_major(_Jtmp, 6, n, _in[5].data());
+    _model->computeJdotQdot(_waist_link, Eigen::Vector3d::Zero(), jdqd);
+    std::memcpy(_in[6].data(), jdqd.data(), sizeof(double) * 6);
     _model->getPose(_waist_link, P);
-    std::memcpy(_in[7].data(), P.m, sizeof(P.m));
-    std::memcpy(_in[8].data(), _waist_ref.m, sizeof(P.m));
+    copy_pose(P, _in[7].data());
+    copy_pose(_waist_ref, _in[8].data());
     for (size_t c = 0; c < nc; ++c) {
-        _model->getJacobian(_contact_links[c], J);
-        copy_row_major(J, 6, n, _in[9].data() + c * 6 * n);
-        _model->computeJdotQdot(_contact_links[c], v);
-        std::memcpy(_in[10].data() + c * 6, v.data(), sizeof(double) * 6);
+        _model->getJacobian(_contact_links[c], _Jtmp);
+        copy_row_major(_Jtmp, 6, n, _in[9].data() + c * 6 * n);
+        _model->computeJdotQdot(_contact_links[c], Eigen::Vector3d::Zero(), jdqd);
+        std::memcpy(_in[10].data() + c * 6, jdqd.data(), sizeof(double) * 6);
         _model->getPose(_contact_links[c], P);
-        std::memcpy(_in[11].data() + c * 12, P.m, sizeof(P.m));
-        std::memcpy(_in[12].data() + c * 12, _feet_ref[c].m, sizeof(P.m));
+        copy_pose(P, _in[11].data() + c * 12);
+        copy_pose(_feet_ref[c], _in[12].data() + c * 12);
     }
     wbq_contact_inputs in{};
     in.batch = 1;
@@ -133,10 +150,12 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
     in.pose_c_ref = _in[12].data();
     const int32_t cm = _cmask;
     in.cmask = &cm;
+
+    /* Solve QP (:188-193) and the ID post-step tau = M qdd + h - sum_c J_c^T w_c (:206-218) */
     int32_t status = WBQ_STATUS_NUMERICAL, iters = 0;
-    Eigen::VectorXd tau(n, 0.0);
+    _x.setZero(_x.size());
     if (wbq_set_contact_inputs(_ctx, &in) != WBQ_SUCCESS || wbq_solve(_ctx) != WBQ_SUCCESS ||
-        wbq_get_outputs(_ctx, tau.data(), &status, &iters) != WBQ_SUCCESS ||
+        wbq_get_outputs(_ctx, _tau.data(), &status, &iters) != WBQ_SUCCESS ||
         wbq_get_contact_outputs(_ctx, _x.data()) != WBQ_SUCCESS)
         status = WBQ_STATUS_NUMERICAL;
     _status = status;
@@ -146,35 +165,39 @@ void ForceAccExample::control_loop(double /*time*/, double /*period*/) // :167-2
         std::fprintf(stderr, "Unable to solve!!!\n");
         return;
     }
-    for (int j = 0; j < n; ++j) _qddot_value[j] = _x[j]; // :196
-    _tau = tau;                                          // ID(q, qd, qdd) - tau_c (:206-218)
-    // logs (:200, :233-236): wrench w_c = [f_c; 0] per contact, tau_c = sum_c J_c^T w_c
-    Eigen::VectorXd tau_c(n, 0.0), w(6, 0.0);
-    for (size_t c = 0; c < nc; ++c) {
-        for (int k = 0; k < 3; ++k) w[k] = _x[n + 3 * c + k];
-        const double *Jc = _in[9].data() + c * 6 * n; // row-major 6 x n
-        for (int k = 0; k < 3; ++k)
-            for (int j = 0; j < n; ++j) tau_c[j] += Jc[k * n + j] * w[k];
-        _logger->add(_contact_links[c] + "_wrench", w);
+
+    /* Retrieve values (:196-201) */
+    for (int j = 0; j < n; ++j) _qddot_value[j] = _x[j];
+    for (size_t i = 0; i < nc; i++) {
+        for (int k = 0; k < 3; ++k) _wrench_value[i][k] = _x[n + 3 * i + k];
+        _logger->add(_contact_links[i] + "_wrench", _wrench_value[i]);
     }
-    _logger->add("tau", _tau);
-    _logger->add("tau_c", tau_c);
+
+    /* Compute torques due to contacts (:206-210), for the log: tau_c = sum_i J_i^T w_i */
+    _tau_c.setZero(_model->getJointNum());
+    for (size_t i = 0; i < nc; i++) {
+        const double *Jc = _in[9].data() + i * 6 * n; // row-major 6 x n
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < n; ++j) _tau_c[j] += Jc[k * n + j] * _wrench_value[i][k];
+    }
+    _model->setJointEffort(_tau); // :219
+
+    _logger->add("tau", _tau); // :233-236
+    _logger->add("tau_c", _tau_c);
     _logger->add("qddot_value", _qddot_value);
     _logger->add("x", _x);
-    _model->setJointEffort(_tau);                        // :219
-    _robot->setStiffness(_k);                            // :239-241 (re-sent every tick)
+
+    /* Send commands to robot (:239-248) */
+    _robot->setStiffness(_k);
     _robot->setDamping(_d);
-    _robot->setReferenceFrom(*_model, XBot::Sync::Position, XBot::Sync::Effort); // :242
-    _robot->move(); // :248
+    _robot->setReferenceFrom(*_model, XBot::Sync::Position, XBot::Sync::Effort);
+    _robot->move();
+    _model->log(_logger, time); // :249
 }
 
-void ForceAccExample::sync_model() // :256-282; floating-base state comes with the model here
+void ForceAccExample::sync_model() // :256-282; the floating-base state comes with the robot state here
 {
-    Eigen::VectorXd v;
-    _robot->getMotorPosition(v);
-    _model->setJointPosition(v);
-    _robot->getMotorVelocity(v);
-    _model->setJointVelocity(v);
+    _model->syncFrom(*_robot);
     _model->update();
 }
 

@@ -1,10 +1,10 @@
 // QPPVMPlugin.cpp -- demo::QPPVMPlugin over libwbq. Mirrors the reference's control flow
-// (src/QPPVMPlugin.cpp), with the OpenSoT/qpOASES solve replaced by one wbq_solve.
+// (src/QPPVMPlugin.cpp) with its own XBotInterface / Eigen / KDL spellings; the OpenSoT task
+// wiring and the qpOASES solve are replaced by one wbq context and one wbq_solve per tick.
 #include <QPPVM_RT_plugin/QPPVMPlugin.h>
 
 #include <cmath>
 #include <cstdio>
-#include <cstring>
 
 #include "abi_copy.h"
 
@@ -19,25 +19,31 @@ QPPVMPlugin::~QPPVMPlugin()
     if (_ctx) wbq_destroy(_ctx);
 }
 
-bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle)
+bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle) // :42-199
 {
-    _robot = handle->getRobotInterface();
     _matlogger = XBot::MatLogger::getLogger(_log_prefix); // :44
-    _model = handle->getModel(); // reference: hard-coded CENTAURO yaml (:50-51)
-    const int n = _model->getJointNum();
-    _matlogger->reserve(30000); // _model->initLog(_matlogger, 30000) (:54)
+    _robot = handle->getRobotInterface();                  // :48
+    // the reference hard-codes a CENTAURO yaml here (:50-51); its commented line :49 takes the
+    // config the handle names, which is what a dummy-mode / test runtime can provide
+    _model = XBot::ModelInterface::getModel(handle->getPathToConfigFile());
+    if (!_model) return false;
+    _model->initLog(_matlogger, 30000); // :54
 
     _model->getEffortLimits(_tau_max_const); // :56-58
-    _tau_min_const.setZero(n);
-    for (int j = 0; j < n; ++j) _tau_min_const[j] = -_tau_max_const[j];
-    _tau_d.setZero(n);
+    _tau_min_const = -_tau_max_const;
+
+    _tau_d.resize(_model->getJointNum()); // :61-62
+    _tau_d.setZero(_tau_d.size());
+    _tau_qp.setZero(_tau_d.size());
+
     _model->computeNonlinearTerm(_h); // :65 (before any sync, as in the reference)
 
     _model->getRobotState("home", _q_home); // :69-72
     _model->setJointPosition(_q_home);
-    _model->setJointVelocity(Eigen::VectorXd(n, 0.0));
+    _model->setJointVelocity(Eigen::VectorXd(_q_home.size()).setConstant(0.0));
     _model->update();
-    _q = _q_home;
+
+    _q = _q_home; // :74-75
     _q_ref = _q;
 
     // robot-side impedance: zero except the wrist joints 5-7 of both arms (:77-96)
@@ -55,8 +61,11 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle)
     }
 
     // task / stack / solver wiring: K = 5, D = 2 (:105-106); Kc = 700, Dc = 70 (:136-137,
-    // :148-149); rows {0,1,2} (:134, :147); ((ee_right + ee_left) / joint) << limits (:177)
-    std::vector<double> Kc(12, 700.0), Dc(12, 70.0), Kq(n, 5.0), Dq(n, 2.0);
+    // :148-149); rows {0,1,2} (:134, :147); ((ee_right + ee_left) / joint) << limits (:177-179);
+    // QPOases_sot(.., 1.0) (:188)
+    const int n = _model->getJointNum();
+    const Eigen::VectorXd Kc = Eigen::VectorXd::Constant(12, 700.0), Dc = Eigen::VectorXd::Constant(12, 70.0);
+    const Eigen::VectorXd Kq = Eigen::VectorXd::Constant(n, 5.0), Dq = Eigen::VectorXd::Constant(n, 2.0);
     wbq_desc d{};
     d.form = WBQ_FORM_QPPVM;
     d.n = n;
@@ -76,6 +85,10 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle)
         std::fprintf(stderr, "QPPVMPlugin: wbq_create failed (%d)\n", rc);
         return false;
     }
+    // the solver's log (:189, :254, :258): variables created here, outside the RT loop
+    _matlogger->createVectorVariable("tau_qp", n, 1, 30000);
+    _matlogger->createVectorVariable("tau_desired", n, 1, 30000);
+    _matlogger->createScalarVariable("time_matlogger", 1, 30000);
     _M.resize((size_t)n * n);
     _J.resize((size_t)2 * 6 * n);
     _pose.resize(24);
@@ -87,36 +100,47 @@ void QPPVMPlugin::on_start(double time) // :261-305
 {
     sense();
     _model->computeNonlinearTerm(_h);
+
     _start_time = time;
     _robot->setStiffness(_k);
     _robot->setDamping(_d);
     _robot->move();
-    // references = current poses and current q (:271-279)
-    for (int t = 0; t < 2; ++t) _model->getPose(_ee_links[t], _ref[t]);
+
+    // references = the current poses and the current q (:271-279)
+    Eigen::Affine3d left_ee_pose;
+    _model->getPose(_ee_links[1], left_ee_pose);
+    Eigen::Affine3d right_ee_pose;
+    _model->getPose(_ee_links[0], right_ee_pose);
+    _ee_ref[1] = left_ee_pose;
+    _ee_ref[0] = right_ee_pose;
     _q_ref = _q;
-    _model->getPose(_ee_links[1], _start_pose); // left end effector (:284)
+
+    _model->getPose(_ee_links[1], _start_pose); // :287
 }
 
-void QPPVMPlugin::QPPVMControl(double time) // :201-259
+void QPPVMPlugin::QPPVMControl(const double time) // :201-259
 {
     const int n = _model->getJointNum();
     if (_set_ref) { // :217-223 -- y += 0.15 sin(t - t0), z += 0.15 (1 - cos(t - t0)) on the left task
-        _ref[1] = _start_pose;
-        _ref[1].m[7] = _start_pose.m[7] + 0.15 * std::sin(time - _start_time);
-        _ref[1].m[11] = _start_pose.m[11] + 0.15 * (1.0 - std::cos(time - _start_time));
+        _ref = _start_pose;
+        _ref.p.y(_start_pose.p.y() + 0.15 * std::sin(time - _start_time));
+        _ref.p.z(_start_pose.p.z() + 0.15 * (1.0 - std::cos(time - _start_time)));
+        for (int r = 0; r < 3; ++r) { // _ee_task_left->setReference(_ref)
+            for (int c = 0; c < 3; ++c) _ee_ref[1].linear()(r, c) = _ref.M(r, c);
+            _ee_ref[1].translation()(r) = _ref.p(r);
+        }
     }
-    Eigen::MatrixXd M, J;
-    // element-wise into the ABI's row-major layout (include/wbq.h): Eigen's MatrixXd is
-    // column-major, so its data() is never copied as is
-    _model->getInertiaMatrix(M);
-    copy_row_major(M, n, n, _M.data());
+    // _autostack->update(_q) (:226): the model quantities the tasks pull, copied element-wise into
+    // the ABI's row-major layout (include/wbq.h; Eigen's MatrixXd is column-major)
+    _model->getInertiaMatrix(_Mtmp);
+    copy_row_major(_Mtmp, n, n, _M.data());
     for (int t = 0; t < 2; ++t) {
-        _model->getJacobian(_ee_links[t], J);
-        copy_row_major(J, 6, n, _J.data() + (size_t)t * 6 * n);
+        _model->getJacobian(_ee_links[t], _Jtmp);
+        copy_row_major(_Jtmp, 6, n, _J.data() + (size_t)t * 6 * n);
         Eigen::Affine3d P;
         _model->getPose(_ee_links[t], P);
-        std::memcpy(_pose.data() + 12 * t, P.m, sizeof(P.m));
-        std::memcpy(_pose_ref.data() + 12 * t, _ref[t].m, sizeof(P.m));
+        copy_pose(P, _pose.data() + 12 * t);
+        copy_pose(_ee_ref[t], _pose_ref.data() + 12 * t);
     }
     wbq_inputs in{};
     in.batch = 1;
@@ -129,33 +153,38 @@ void QPPVMPlugin::QPPVMControl(double time) // :201-259
     in.qd = _dq.data();
     in.qref = _q_ref.data();
     in.h = _h.data();
-    int32_t status = 3, iters = 0;
-    _tau_d.setZero(n);
+    int32_t status = WBQ_STATUS_NUMERICAL, iters = 0;
+    // solver->solve(_tau_d) (:246) and _tau_d + _h (:256) in one call: wbq returns tau = tau_qp + h
     if (wbq_set_inputs(_ctx, &in) != WBQ_SUCCESS || wbq_solve(_ctx) != WBQ_SUCCESS ||
         wbq_get_outputs(_ctx, _tau_d.data(), &status, &iters) != WBQ_SUCCESS) {
         status = WBQ_STATUS_NUMERICAL;
-        for (int j = 0; j < n; ++j) _tau_d[j] = _h[j];
+        _tau_d = _h;
     }
     _status = status;
     _iters = iters;
-    if (status != WBQ_STATUS_OK) { // :246-249 -- tau_qp = 0, i.e. tau = h (already in tau)
+    if (status != WBQ_STATUS_OK) { // :246-249 -- tau_qp = 0, i.e. tau = h (what wbq returned)
         ++_solver_errors;
         std::fprintf(stderr, "SOLVER ERROR!\n");
     }
-    Eigen::VectorXd tau_qp(n, 0.0);
-    for (int j = 0; j < n; ++j) tau_qp[j] = _tau_d[j] - _h[j];
-    _matlogger->add("tau_qp", tau_qp);       // :254
+    _tau_qp = _tau_d;
+    _tau_qp -= _h;
+    _matlogger->add("tau_qp", _tau_qp);       // :254
     _matlogger->add("tau_desired", _tau_d); // :258
 }
 
-void QPPVMPlugin::control_loop(double time, double /*period*/) // :308-329
+void QPPVMPlugin::control_loop(double time, double period) // :308-329
 {
+    (void)period;
     sense();
     _model->computeNonlinearTerm(_h);
+
     QPPVMControl(time);
+
+    // set the joint effort on the model and then synchronize the effort on the robot
     _model->setJointEffort(_tau_d);
     _robot->setReferenceFrom(*_model, XBot::Sync::Effort);
     _matlogger->add("time_matlogger", time); // :322
+    _model->log(_matlogger, time);           // :325
     _robot->move();
 }
 
@@ -176,12 +205,13 @@ bool QPPVMPlugin::close() // :339-342 (the reference is missing its return)
     return true;
 }
 
-void QPPVMPlugin::syncFromMotorSide(XBot::RobotInterface::Ptr robot, XBot::ModelInterface::Ptr model)
+void QPPVMPlugin::syncFromMotorSide(XBot::RobotInterface::Ptr robot, XBot::ModelInterface::Ptr model) // :344-353
 {
-    Eigen::VectorXd v;
-    robot->getMotorPosition(v);
-    model->setJointPosition(v);
-    robot->getMotorVelocity(v);
-    model->setJointVelocity(v);
+    robot->getMotorPosition(_jidmap);
+    model->setJointPosition(_jidmap);
+
+    robot->getMotorVelocity(_jidmap);
+    model->setJointVelocity(_jidmap);
+
     model->update();
 }

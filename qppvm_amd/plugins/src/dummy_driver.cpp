@@ -36,6 +36,7 @@ static std::string tick_percentiles(std::vector<double> us)
 static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, const char *log_prefix)
 {
     auto handle = std::make_shared<dummy::Handle>(dummy::quadruped(n));
+    handle->register_model();
     XBotPlugin::ForceAccExample plugin;
     if (log_prefix) plugin.set_log_prefix(log_prefix);
     if (!plugin.init_control_plugin(handle)) {
@@ -45,7 +46,7 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, cons
     FILE *f = dump ? std::fopen(dump, "wb") : nullptr;
     const double dt = 1e-3;
     {
-        Eigen::VectorXd q(n, 0.0), qd(n, 0.0);
+        Eigen::VectorXd q = Eigen::VectorXd::Zero(n), qd = Eigen::VectorXd::Zero(n);
         for (int j = 0; j < n; ++j) qd[j] = 0.1 * ((j % 5) - 2);
         handle->robot().set_state(q, qd);
     }
@@ -114,6 +115,7 @@ int main(int argc, char **argv)
     prm.n = n;
     if (stress) prm.jscale = 0.5;
     auto handle = std::make_shared<dummy::Handle>(prm);
+    handle->register_model();
     demo::QPPVMPlugin plugin;
     if (log_prefix) plugin.set_log_prefix(log_prefix);
     plugin.set_reference_trajectory(set_ref);
@@ -133,13 +135,15 @@ int main(int argc, char **argv)
         std::fwrite(q.data(), sizeof(double), n, f);
         for (const char *link : {"arm2_7", "arm1_7"}) {
             Eigen::Affine3d P;
+            double pm[12];
             handle->model().getPose(link, P);
-            std::fwrite(P.m, sizeof(double), 12, f);
+            copy_pose(P, pm);
+            std::fwrite(pm, sizeof(double), 12, f);
         }
     }
     // the references are the start posture; kick the robot so the tasks have work to do
     {
-        Eigen::VectorXd q(n, 0.0), qd(n, 0.0);
+        Eigen::VectorXd q = Eigen::VectorXd::Zero(n), qd = Eigen::VectorXd::Zero(n);
         for (int j = 0; j < n; ++j) qd[j] = 0.2 * ((j % 7) - 3);
         handle->robot().set_state(q, qd);
     }
@@ -176,8 +180,10 @@ int main(int argc, char **argv)
             }
             for (const char *link : {"arm2_7", "arm1_7"}) {
                 Eigen::Affine3d P;
+                double pm[12];
                 m.getPose(link, P);
-                std::fwrite(P.m, sizeof(double), 12, f);
+                copy_pose(P, pm);
+                std::fwrite(pm, sizeof(double), 12, f);
             }
             std::fwrite(q.data(), sizeof(double), n, f);
             std::fwrite(qd.data(), sizeof(double), n, f);

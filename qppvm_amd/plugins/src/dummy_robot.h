@@ -123,10 +123,10 @@ public:
         return true;
     }
     // d/dt (J) qd with J_rc = J0_rc (1 + 0.1 cos q_c): sum_c -0.1 J0_rc sin(q_c) qd_c^2
-    bool computeJdotQdot(const std::string &link, Eigen::VectorXd &jdqd) const override
+    bool computeJdotQdot(const std::string &link, const Eigen::Vector3d &, Eigen::Vector6d &jdqd) const override
     {
         const int t = task(link);
-        jdqd.setZero(6);
+        jdqd.setZero();
         for (int r = 0; r < 6; ++r)
             for (int c = 0; c < n_; ++c) jdqd[r] -= 0.1 * J0_[t][r * n_ + c] * std::sin(q_[c]) * qd_[c] * qd_[c];
         return true;
@@ -141,7 +141,7 @@ public:
                 p += 0.05 * J0_[t][k * n_ + c] * std::sin(q_[c]);
                 s += 0.05 * J0_[t][(3 + k) * n_ + c] * std::sin(q_[c]);
             }
-            T.m[4 * k + 3] = p;
+            T.translation()(k) = p;
             w[k] = s;
         }
         // rotation exp([w]x) (Rodrigues)
@@ -153,7 +153,7 @@ public:
             for (int c = 0; c < 3; ++c) {
                 double kk = 0.0;
                 for (int m = 0; m < 3; ++m) kk += K[r][m] * K[m][c];
-                T.m[4 * r + c] = (r == c ? 1.0 : 0.0) + a * K[r][c] + b * kk;
+                T.linear()(r, c) = (r == c ? 1.0 : 0.0) + a * K[r][c] + b * kk;
             }
         return true;
     }
@@ -175,7 +175,11 @@ private:
 
 class Robot : public XBot::RobotInterface {
 public:
-    explicit Robot(int n) : n_(n), q_(n, 0.0), qd_(n, 0.0), k_(n, 500.0), d_(n, 10.0) {}
+    explicit Robot(int n)
+        : n_(n), q_(Eigen::VectorXd::Zero(n)), qd_(Eigen::VectorXd::Zero(n)), k_(Eigen::VectorXd::Constant(n, 500.0)),
+          d_(Eigen::VectorXd::Constant(n, 10.0))
+    {
+    }
     int getJointNum() const override { return n_; }
     int getDofIndex(const std::string &joint) const override
     {
@@ -268,7 +272,17 @@ public:
     explicit Handle(const Params &p) : model_(std::make_shared<Model>(p)), robot_(std::make_shared<Robot>(p.n)) {}
     std::string getPathToConfigFile() const override { return "dummy://synthetic"; }
     XBot::RobotInterface::Ptr getRobotInterface() override { return robot_; }
-    XBot::ModelInterface::Ptr getModel() override { return model_; }
+    // the model XBot::ModelInterface::getModel(path) hands the plugin: the driver (the XBotCore
+    // stand-in) registers it as the loader for this handle's config path
+    std::shared_ptr<Model> model_ptr() { return model_; }
+    void register_model()
+    {
+        auto m = model_;
+        const std::string path = getPathToConfigFile();
+        XBot::ModelInterface::setModelLoader([m, path](const std::string &p) {
+            return p == path ? XBot::ModelInterface::Ptr(m) : XBot::ModelInterface::Ptr();
+        });
+    }
     Model &model() { return *model_; }
     Robot &robot() { return *robot_; }
 

@@ -89,9 +89,12 @@ def test_plugin_shells_export_factories():
     CMakeLists.txt:48-49) build with g++ against the compat XCM header and export the
     REGISTER_XBOT_PLUGIN factory symbols XBotCore dlopens."""
     plugin, driver, forceacc = wbq_build.build_plugins()
-    for lib, cls in ((plugin, "QPPVMPlugin"), (forceacc, "ForceAccExample")):
+    # REGISTER_XBOT_PLUGIN(QPPVMPlugin, ..) (QPPVMPlugin.cpp:29) names its factory pair;
+    # REGISTER_XBOT_PLUGIN_(XBotPlugin::ForceAccExample) (ForceAcc.cpp:26) emits the fixed pair
+    for lib, syms in ((plugin, ("create_instance_QPPVMPlugin", "destroy_instance_QPPVMPlugin")),
+                      (forceacc, ("create_instance", "destroy_instance"))):
         out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
-        for sym in (f"create_instance_{cls}", f"destroy_instance_{cls}"):
+        for sym in syms:
             assert re.search(rf"\bT {sym}$", out, re.M), (lib, sym)
     assert os.access(driver, os.X_OK)
 
