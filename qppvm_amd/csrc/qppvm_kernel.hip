@@ -337,18 +337,12 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     }
 }
 
-// With WBQ_INLINE_REPAIR: inlined (a real call, noinline, slowed the whole fast kernel:
-// profiles/r02_v5_ab_noinline_c1.log).
-#ifndef WBQ_REPAIR_INLINE
-#define WBQ_REPAIR_INLINE __forceinline__
-#endif
 // Level-0 repair of one instance (the lanes with rep set; every lane of the wave calls it):
 // y* by BVLS, the pins, and a fresh dual active set (or, when the pinned level-0 point is the
 // only feasible one, that point) -> tau, status, iters, warm-start hint. S is the instance's
-// active-set LDS. Shared by the repair kernel (n > 32) and the fast kernel for n <= 32 (there a
-// solve is one launch).
+// active-set LDS.
 template <int NP, int M0>
-__device__ WBQ_REPAIR_INLINE void repair_instance(const QppvmArgs &a, double *S, long b, int i, bool rep)
+__device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, long b, int i, bool rep)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int n = a.n;
@@ -388,7 +382,7 @@ __device__ WBQ_REPAIR_INLINE void repair_instance(const QppvmArgs &a, double *S,
     }
 }
 
-// Level-0 repair kernel (n > 32): instances with status -2 (flagged by the fast kernel, or by
+// Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by
 // the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set.
 template <int NP, int M0>
 __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
@@ -413,18 +407,6 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
         repair_instance<NP, M0>(a, S, b, i, valid);
     }
 }
-
-// The level-0 repair inside the fast kernel (n <= 32, WBQ_INLINE_REPAIR builds) saves the
-// follow-up launch but its register demand spills into the fast path: A/B on one box
-// (profiles/r02_v8_ab_*) config 1 113.7 M QP/s inlined vs 115.2 M as the separate kernel,
-// config 2 14.2 M vs 17.8 M. Off by default.
-#ifdef WBQ_INLINE_REPAIR
-template <int NP, int M0>
-constexpr bool kInlineRepair = NP == 32 && M0 <= 6;
-#else
-template <int NP, int M0>
-constexpr bool kInlineRepair = false;
-#endif
 
 // Waves per SIMD of the n > 32 fast kernel (template W). W = 2 caps it at 256 registers (it
 // spills, ~760 B of scratch per lane) but doubles the resident instances: A/B n = 39 config 1
@@ -727,12 +709,9 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
                     a.iters[b] = it2;
                 }
             }
-            if constexpr (kInlineRepair<NP, M0>) {
-                if (__any(rep)) { // the level-0 repair right here (wave-uniform branch)
-                    __syncthreads();
-                    repair_instance<NP, M0>(a, S, b, i, rep);
-                }
-            } else if (rep && i == 0) {
+            // the level-0 repair runs in its own kernel: inlined here its register demand spilled
+            // into the fast path
+            if (rep && i == 0) {
                 a.status[b] = -2; // qppvm_repair_kernel
                 wl_push(a, 1, b);
             }
@@ -792,12 +771,7 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     // follow-up kernels: grid-stride over their work lists, at most kFollowGrid blocks
     const unsigned fgrid = grid < kFollowGrid ? grid : kFollowGrid;
-    if constexpr (kInlineRepair<NP, M0>) {
-        // active set and level-0 repair run inside the fast kernel: one launch per solve, the
-        // work lists are unused
-        (void)fgrid;
-        return hipSuccess;
-    } else if constexpr (MERGED) {
+    if constexpr (MERGED) {
         return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
     } else {
         e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream);

@@ -548,9 +548,6 @@ __device__ __forceinline__ void wl_push(const QppvmArgs &a, int list, long b)
 // Follow-up grid cap: 2 waves per SIMD over the whole chip (launch cost measured independent of
 // the grid size, scripts/launch_probe.hip; a smaller cap starves a solve where many instances
 // need the repair, e.g. diverging MPC rollouts)
-#ifndef WBQ_FOLLOW_GRID
-#define WBQ_FOLLOW_GRID 2048
-#endif
-constexpr unsigned kFollowGrid = WBQ_FOLLOW_GRID;
+constexpr unsigned kFollowGrid = 2048;
 
 }  // namespace wbq
