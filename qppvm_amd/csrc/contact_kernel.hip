@@ -821,8 +821,10 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
     if (L.NR > NRC * ((NQ == 64 && TR) ? 2 : 1) || L.ME > 64 || L.NX > 64) return hipErrorInvalidValue;
     if (!TR && L.ME > KMR) return hipErrorInvalidValue; // the register slot vectors hold every active row
     const size_t lds = sizeof(double) * L.SIZE;
-    const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR>, lds);
-    if (e != hipSuccess) return e;
+    if (a.prepare) {
+        const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR>, lds);
+        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR>, lds);
+    }
     hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess || !a.wl) return e2;
@@ -830,8 +832,6 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
         e2 = hipEventRecord(mid, stream);
         if (e2 != hipSuccess) return e2;
     }
-    e2 = ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR>, lds);
-    if (e2 != hipSuccess) return e2;
     const unsigned grid = a.B < (int)kContactRepairGrid ? (unsigned)a.B : kContactRepairGrid;
     hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR>), dim3(grid), dim3(64), lds, stream, a);
     return hipGetLastError();

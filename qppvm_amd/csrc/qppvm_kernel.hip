@@ -337,6 +337,25 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     }
 }
 
+// u = M^-1 x (lane i: x_i in, u_i out; lanes with row unset carry identity rows): block
+// Gauss-Jordan on M's rows reloaded from HBM/L2, the QA region as its panel scratch (rare path)
+template <int NP>
+__device__ double minv_apply(const QppvmArgs &a, double *S, const ActiveLayout<NP> &L, long b, int i, bool row, double x)
+{
+    const int n = a.n;
+    const int ic = i < n ? i : n - 1;
+    const double *Mb = a.M + b * n * n + ic; // (64-bit addressing: instances from a work list)
+    double A[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+    double rhs[1] = {row ? x : 0.0};
+    __syncthreads();
+    (void)block_gj<NP, 1, 1>(A, rhs, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
+    return rhs[0];
+}
+
 // Level-0 repair of one instance (the lanes with rep set; every lane of the wave calls it):
 // y* by BVLS, the pins, and a fresh dual active set (or, when the pinned level-0 point is the
 // only feasible one, that point) -> tau, status, iters, warm-start hint. S is the instance's
@@ -354,14 +373,22 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     WBQ_STAMP(11);
     int status = ro.status, iters = 0;
     bool infeasible = false;
-    // level 1 over a single feasible point needs no active set (rollouts do: they integrate
-    // u = M^-1 x, which the active set leaves in LDS)
-    const bool uniq = ro.unique && !a.integrate;
+    // level 1 over a single feasible point needs no active set: x = x*. (The active set on that
+    // point is degenerate by construction -- the pins and G u = y* are dependent -- and could end
+    // with "no step", status 2: the config-4 rollouts once did, scripts/diag_mpc.py.)
+    const bool uniq = ro.unique;
+    const ActiveLayout<NP> L(a.ntasks, a.m0);
     double x_i = ro.x;
     if (__any(rep && !uniq))
         x_i = gi_solve<NP, M0>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
                                infeasible);
     if (uniq) x_i = ro.x;
+    if (a.integrate && __any(rep && uniq)) { // rollouts integrate qdd = u = M^-1 x*
+        const bool r2 = row && uniq;
+        const double u2 = minv_apply<NP>(a, S, L, b, i, r2, ro.x);
+        if (rep && uniq) S[L.U + i] = u2;
+        __syncthreads();
+    }
     WBQ_STAMP(12);
 #ifdef WBQ_STAMPS
     if (threadIdx.x == 0 && a.stamps) { // step counts of the diagnostic build
@@ -374,7 +401,7 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
     if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
     if (row) a.tau[b * n + i] = tau_i;
-    rollout_step(a, b, i, row, S[ActiveLayout<NP>(a.ntasks, a.m0).U + i], status == 0);
+    rollout_step(a, b, i, row, S[L.U + i], status == 0);
     if (rep && (i & (NP - 1)) == 0) {
         a.status[b] = status;
         a.iters[b] = iters + ro.it;
@@ -737,8 +764,7 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
 {
     constexpr int IPW = kWave / NP;
     const size_t lds = sizeof(double) * Lay(a.ntasks, a.m0).SIZE * IPW;
-    const hipError_t e = ensure_dynamic_lds((const void *)kern, lds);
-    if (e != hipSuccess) return e;
+    if (a.prepare) return ensure_dynamic_lds((const void *)kern, lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, a);
     return hipGetLastError();
 }
@@ -757,15 +783,22 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
                           : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 2, 32>, a, grid, stream);
     } else if (a.ntasks > 2) {
         e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 1, 64>, a, grid, stream);
-    } else if (a.n <= 40) { // CENTAURO-sized (n = 39)
-        e = a.B > kNp64OneRound ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 40>, a, grid, stream)
-                                : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 40>, a, grid, stream);
     } else {
-        e = a.B > kNp64OneRound ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 64>, a, grid, stream)
-                                : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 64>, a, grid, stream);
+        // W by batch size (both prepared): 2 waves per SIMD above one wave round
+        const bool two = a.B > kNp64OneRound;
+        e = hipSuccess;
+        if (a.n <= 40) { // CENTAURO-sized (n = 39)
+            if (two || a.prepare) e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 40>, a, grid, stream);
+            if (e == hipSuccess && (!two || a.prepare))
+                e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 40>, a, grid, stream);
+        } else {
+            if (two || a.prepare) e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 64>, a, grid, stream);
+            if (e == hipSuccess && (!two || a.prepare))
+                e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 1, 64>, a, grid, stream);
+        }
     }
     if (e != hipSuccess) return e;
-    if (mid) { // end of the dominant launch
+    if (mid && !a.prepare) { // end of the dominant launch
         e = hipEventRecord(mid, stream);
         if (e != hipSuccess) return e;
     }

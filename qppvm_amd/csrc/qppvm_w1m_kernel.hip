@@ -133,7 +133,7 @@ struct W1mGi {
 // level-0 targets from the RepairIn block at R instead of tau_min/max and b0.
 template <int NQ, int M0, int TM>
 __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b, int i, const double *R, int it0,
-                                          int st0)
+                                          int st0, bool l0inf = false)
 {
     constexpr int NRC = 1 + M0; // Gauss-Jordan right-hand sides: tau_imp, G^T
     const int T = a.ntasks, n = a.n, m0 = a.m0;
@@ -403,6 +403,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     if (i == 0) {
         a.status[b] = status;
         a.iters[b] = it0 + gs.iters;
+        a.ws_hint[b] = l0inf ? 1 : 0; // wbq_get_warmstart_hints: this solve needed the level-0 repair
     }
 }
 
@@ -446,6 +447,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
             if (i == 0) {
                 a.status[b] = status;
                 a.iters[b] = ro.it;
+                a.ws_hint[b] = ro.l0inf ? 1 : 0;
             }
             continue;
         }
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
             R[RepairIn::YS + i] = y;
         }
         __syncthreads();
-        w1m_solve<NQ, M0, TM>(a, smem, b, i, R, ro.it, ro.status);
+        w1m_solve<NQ, M0, TM>(a, smem, b, i, R, ro.it, ro.status, ro.l0inf);
     }
 }
 
@@ -477,19 +479,19 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     const W1mLayout L(a.n, a.ntasks, a.m0, NQ, 1 + M0);
     if (L.ME > 64) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
-    hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0, TM>, lds);
-    if (e != hipSuccess) return e;
+    const int ws = ActiveLayout<64>(a.ntasks, a.m0).SIZE;
+    const size_t lds2 = sizeof(double) * ((ws > L.SIZE ? ws : L.SIZE) + RepairIn::SIZE);
+    if (a.prepare) {
+        const hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0, TM>, lds);
+        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)qppvm_w1m_repair_kernel<NQ, M0, TM>, lds2);
+    }
     hipLaunchKernelGGL((qppvm_w1m_kernel<NQ, M0, TM>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (mid) {
         e = hipEventRecord(mid, stream);
         if (e != hipSuccess) return e;
     }
-    const int ws = ActiveLayout<64>(a.ntasks, a.m0).SIZE;
-    const size_t lds2 = sizeof(double) * ((ws > L.SIZE ? ws : L.SIZE) + RepairIn::SIZE);
-    e = ensure_dynamic_lds((const void *)qppvm_w1m_repair_kernel<NQ, M0, TM>, lds2);
-    if (e != hipSuccess) return e;
     const unsigned grid = a.B < (int)kFollowGrid ? (unsigned)a.B : kFollowGrid;
     hipLaunchKernelGGL((qppvm_w1m_repair_kernel<NQ, M0, TM>), dim3(grid), dim3(64), lds2, stream, a);
     return hipGetLastError();

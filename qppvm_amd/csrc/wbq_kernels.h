@@ -51,12 +51,17 @@ struct QppvmArgs {
     // and semi-implicit Euler on q, qd in place
     int integrate;
     double dt;
+    // 1: the launcher raises the dynamic-LDS limit of every kernel variant this configuration can
+    // launch (any batch size) and launches nothing. wbq_create does this once, so a solve takes no
+    // lock and never allocates (include/wbq.h: wbq_solve is RT-safe)
+    int prepare;
 };
 
 constexpr int kStamps = 20; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12
 
 // Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
-// device and kernel; thread-safe: contexts on several devices or threads share it).
+// device and kernel; thread-safe: contexts on several devices or threads share it). Called only
+// by the launchers' prepare pass (wbq_create*), never on the solve path.
 hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes);
 
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
@@ -98,6 +103,7 @@ struct ContactArgs {
     int *work;       // [2][2]
     int *wl;         // [B]
     int epoch;
+    int prepare;     // as QppvmArgs::prepare
 };
 
 // Semi-implicit Euler of one joint of instance b in place (lane i owns joint i of its

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -66,6 +67,24 @@ class ContactInputs(ctypes.Structure):
 _lib = None
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7, as
+    /opt/rocm's): whichever copy loads first serves every later user of that soname. If libwbq
+    pulled /opt/rocm's copy in first, a later `import torch` would find that runtime already in the
+    process and see no GPU. So when torch is installed, its copy is loaded here by path -- without
+    importing torch -- and libwbq, torch tensors and torch streams share it; without torch,
+    /opt/rocm's copy is the runtime."""
+    if "torch" in sys.modules:  # its runtime is in the process already
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    rt = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
 def load_library(path: str = LIB_PATH):
     """Load libwbq.so; raises WbqError (never falls back) when it is missing."""
     global _lib
@@ -73,14 +92,7 @@ def load_library(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise WbqError(f"{path} not built: run `python -m qppvm_amd.build` (hipcc, gfx950)")
-    try:
-        # One HIP runtime per process: torch ships its own libamdhip64 / libhsa-runtime64 with the
-        # same sonames as /opt/rocm's. Loaded first, torch's copies also serve libwbq, so torch
-        # tensors, streams and libwbq contexts share one runtime; loaded second, torch finds
-        # /opt/rocm's runtime already in the process and sees no GPU.
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_hip_runtime()
     lib = ctypes.CDLL(path)
     P, I = ctypes.c_void_p, ctypes.c_int
     lib.wbq_create.argtypes = [ctypes.POINTER(Desc), I, ctypes.POINTER(P)]

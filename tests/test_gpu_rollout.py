@@ -109,3 +109,44 @@ def test_set_state_restarts_rollout(wbq_mod):
     s.close()
     assert rel_err(q1, q2) <= 1e-12 and rel_err(qd1, qd2) <= 1e-12
     assert rel_err(tau1, tau2) <= 1e-9
+
+
+def test_rollout_config4_full_size_properties(wbq_mod, oracle_lib):
+    """The bench's config-4 workload at full size (4096 plant-scaled rollouts x N = 20, limits at
+    the 80 % quantile, repeated from the reset state so the warm start carries over, as bench.py
+    runs it): every step of every rollout ends with status 0 -- the level-0 repair's single-point
+    case once ended at "no step" (status 2) inside rollouts (scripts/diag_mpc.py) -- and the last
+    step's torques carry the KAT-4 certificates (tests/kkt.py): every instance whose last solve
+    went through the level-0 repair, plus 128 others."""
+    import kkt
+    n, B, H, dt = 30, 4096, 20, 1e-3
+    inp = qppvm_instances(QPPVMProblem(n=n), B, seed=1, plant=True)
+    free = wbq_mod.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B)
+    tau_free, _, _ = free.solve_batch(inp)
+    free.close()
+    prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
+    s = wbq_mod.QPPVMSolver(prob, max_batch=B)
+    try:
+        s.set_inputs(inp)
+        repaired = 0
+        for rep in range(2):
+            s.set_state(inp["q"], inp["qd"])
+            for k in range(H):
+                if k == H - 1:
+                    q_last, qd_last = s.state()
+                s.rollout(1, dt)
+                tau, st, _ = s.outputs()
+                assert np.all(st == 0), (rep, k, np.bincount(st))
+                hints = s.warm_hints()
+                repaired += int(hints.sum())
+        q, qd = s.state()
+    finally:
+        s.close()
+    assert repaired > 0  # the repair path runs along the rollouts
+    assert np.all(np.isfinite(q)) and np.all(np.isfinite(qd))
+    last = dict(inp, q=q_last, qd=qd_last)
+    rng = np.random.default_rng(0)
+    check = set(np.where(hints != 0)[0].tolist()) | set(rng.choice(B, 128, replace=False).tolist())
+    for b in sorted(check):
+        c = kkt.qppvm_certificate(oracle_lib, prob, last, b, tau[b])
+        assert max(c["primal"], c["level0"], c["stat"], c["sign"]) <= 1e-9, (b, c)
