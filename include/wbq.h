@@ -104,6 +104,14 @@ typedef struct {
     const double *Dq;  /* [n] joint damping (reference 2) */
     const double *tau_max; /* [n] effort limits */
     const double *tau_min; /* [n] (reference: -tau_max, QPPVMPlugin.cpp:58) */
+    /* JointLimits toggle (OpenSoT torque::JointLimits, built at QPPVMPlugin.cpp:169-171 with gains
+     * k0*10, d0*20; commented out of the reference stack). 1: every instance's box also holds the
+     * joint-limit barrier  Kjl (q_min - q) - Djl qd <= tau <= Kjl (q_max - q) - Djl qd  (the
+     * build's written spec of the [upstream] task; an instance whose box empties is infeasible,
+     * status 2). 0: torque limits only (the reference stack). */
+    int joint_limits;
+    const double *q_min, *q_max; /* [n] joint position limits (ModelInterface::getJointLimits) */
+    const double *Kjl, *Djl;     /* [n] barrier stiffness / damping */
 } wbq_desc;
 
 typedef struct {

@@ -32,7 +32,9 @@ class _Desc(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("ntasks", ctypes.c_int), ("row_mask", ctypes.c_int * 4),
                 ("select_mode", ctypes.c_int), ("joint_weight", ctypes.c_int),
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
-                ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+                ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
+                ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p)]
 
 
 class _Inst(ctypes.Structure):
@@ -85,6 +87,11 @@ def _desc(prob):
     keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
             for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
     d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [a.ctypes.data for a in keep]
+    if getattr(prob, "joint_limits", False):
+        jl = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64) for k in ("q_min", "q_max", "Kjl", "Djl")]
+        keep += jl
+        d.joint_limits = 1
+        d.q_min, d.q_max, d.Kjl, d.Djl = [a.ctypes.data for a in jl]
     return d, keep
 
 

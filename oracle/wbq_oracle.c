@@ -334,10 +334,18 @@ int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *
         for (int k = 0; k < n; ++k) s += tmp[k * n + i] * b1[k];
         g1[i] = -s;
     }
-    /* ---- torque limits shifted by -h (QPPVMPlugin.cpp:66-67, 203-205) */
+    /* ---- torque limits shifted by -h (QPPVMPlugin.cpp:66-67, 203-205), and with the JointLimits
+     * toggle (:169-171) the joint-limit barrier Kjl (q_lim - q) - Djl qd on tau as well */
     for (int j = 0; j < n; ++j) {
-        lb[j] = d->tau_min[j] - in->h[j];
-        ub[j] = d->tau_max[j] - in->h[j];
+        double lo = d->tau_min[j], hi = d->tau_max[j];
+        if (d->joint_limits) {
+            const double bl = d->Kjl[j] * (d->q_min[j] - in->q[j]) - d->Djl[j] * in->qd[j];
+            const double bu = d->Kjl[j] * (d->q_max[j] - in->q[j]) - d->Djl[j] * in->qd[j];
+            lo = bl > lo ? bl : lo;
+            hi = bu < hi ? bu : hi;
+        }
+        lb[j] = lo - in->h[j];
+        ub[j] = hi - in->h[j];
     }
 done:
     free(Minv);

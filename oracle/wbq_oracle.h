@@ -69,6 +69,10 @@ typedef struct {
     const double *Dq;                /* [n] joint damping */
     const double *tau_max;           /* [n] */
     const double *tau_min;           /* [n] */
+    /* JointLimits toggle (QPPVMPlugin.cpp:169-171; include/wbq.h): the box on tau also holds
+     * Kjl (q_min - q) - Djl qd <= tau <= Kjl (q_max - q) - Djl qd */
+    int joint_limits;
+    const double *q_min, *q_max, *Kjl, *Djl; /* [n] */
 } wbq_ref_desc;
 
 /* One instance (all row-major fp64):

@@ -645,7 +645,25 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     GA.zero_from(0);
     gs = GiState();
     gs.status = notspd ? 3 : (a.limits_crossed ? 2 : (l0cap ? 1 : 0));
-    if (gs.status == 0) {
+    // rank cap of the loop: the rows never touch the forces of inactive contacts (their rows
+    // are disabled, their joint-row coefficients zero), so the rows span at most
+    // n + 3 * (active contacts) dimensions, not nx
+    const int dim = n + 3 * __popc((unsigned)cm & ((1u << nc) - 1u));
+    ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, dim};
+    if constexpr (TR) {
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
+    }
+    const GiVecs gv{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, SREG ? KMR + 1 : L.TS};
+    bool warm = false;
+    if constexpr (!REPAIR) { // the last solve's final active set in one batch (dual_gi.h warm_start)
+        if (gs.status == 0 && a.ws_rows) {
+            const int wsg = kind == 2 ? (int)a.ws_rows[b * 64 + i] : 0;
+            const bool iseq = kind == 1;
+            warm = warm_start<KM>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, iseq, wsg);
+        }
+    }
+    if (gs.status == 0 && !warm) {
         // The 12 equality rows in one batch. Lane r < 12 holds row r of Gamma_EE; a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane
         // c then forward-substitutes column c of T = L^-1 against the broadcast rows of L, and
@@ -716,20 +734,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
         __syncthreads();
     }
-    {
-        // rank cap of the loop: the rows never touch the forces of inactive contacts (their rows
-        // are disabled, their joint-row coefficients zero), so the rows span at most
-        // n + 3 * (active contacts) dimensions, not nx
-        const int dim = n + 3 * __popc((unsigned)cm & ((1u << nc) - 1u));
-        ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, dim};
-        if constexpr (TR) {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
-        }
-        dual_gi<KM>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, SREG ? KMR + 1 : L.TS}, i, Trow, Tcol, GA, kind,
-                    lo, hi, nrm, s_i, gs,
-                    a.max_iter);
-    }
+    dual_gi<KM>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs, a.max_iter);
     if (gs.status != 1 && gs.status != 3) break;
     }
     int status = gs.status;
@@ -754,6 +759,11 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     __syncthreads();
     WBQ_STAMP(5);
     const bool ok = status == 0;
+    if (a.ws_rows) { // the next solve's warm start: this solve's final active set (a repaired solve's
+                     // pinned problem is not the next solve's: cold then)
+        const int wrec = warm_record(S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS}, i, gs);
+        a.ws_rows[b * 64 + i] = (signed char)((ok && !REPAIR && kind == 2) ? wrec : 0);
+    }
     double tau_i = h_i;
     if (ok && qrow) { // joint row i: M_i qdd - J_c,i^T f + h_i
         double t = h_i;

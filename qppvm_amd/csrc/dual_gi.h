@@ -296,6 +296,92 @@ __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k,
     }
 }
 
+// Warm start (the qpOASES hot-start analogue, SURVEY.md 8b ownership row): the equality rows
+// (iseq) and the inequality rows the previous solve of this instance ended with active (wsgn =
+// their side, +1 lower / -1 upper; 0 none) enter the active set in one batch -- slot order:
+// equalities, then the warm rows, each by row index. Gamma_AA is factored from scratch
+// (refactor_T), lambda_A = T^T T (b_A - s_A), and the batch is kept only if it is dual feasible
+// (every inequality multiplier >= 0, clamped at roundoff) and well conditioned (relative pivots
+// above 1e-12); the dual loop then continues from it as from any of its own states. Otherwise
+// nothing is changed and the caller starts cold. A warm start changes the path, never the
+// solution: the loop still adds every violated row and drops every blocking one.
+template <int KM, class P, class TrowT, class TcolT, class GAT>
+__device__ bool warm_start(const P &pb, double *S, const GiVecs &V, int i, TrowT &Trow, TcolT &Tcol, GAT &GA,
+                           int kind, double lo, double hi, double &s_i, GiState &g, bool iseq, int wsgn)
+{
+    const bool isw = !iseq && kind == 2 && wsgn != 0;
+    const unsigned long long me = __ballot(iseq), mw = __ballot(isw);
+    const unsigned long long below = i == 0 ? 0ull : (~0ull >> (64 - i));
+    const int ne = __popcll(me), k = ne + __popcll(mw);
+    if (__popcll(mw) == 0 || k > KM || k > pb.dim) return false;
+    const int slot = iseq ? __popcll(me & below) : (isw ? ne + __popcll(mw & below) : -1);
+    if (slot >= 0) {
+        S[V.AC + slot] = (double)i;
+        S[V.WV + slot] = iseq ? 1.0 : (double)wsgn;
+    }
+    __syncthreads();
+    GiState w;
+    w.status = g.status;
+    if (i < k) {
+        w.act = (int)S[V.AC + i];
+        w.sgn = S[V.WV + i];
+        w.aeq = i < ne;
+    }
+    refactor_T(pb, S, V.TB, V.TST, i, k, w);
+    // conditioning: the relative pivot d^2 / Gamma_pp = 1 / (T_aa^2 Gamma_pp) of every slot
+    const double taa = i < k ? S[V.TB + i * V.TST + i] : 1.0;
+    const double piv = i < k ? 1.0 / (taa * taa * pb.gamma(w.act, w.act)) : kInf;
+    // (every lane takes part in every shuffle: a shuffle under a divergent branch reads lanes
+    // that did not execute it)
+    const double lo_a = __shfl(lo, w.act), hi_a = __shfl(hi, w.act), s_a = __shfl(s_i, w.act);
+    const double ye = i < k ? w.sgn * ((w.sgn > 0.0 ? lo_a : hi_a) - s_a) : 0.0;
+    S[V.VV + i] = ye;
+    Trow.load_factor(S + V.TB, V.TST, i, k, false);
+    Tcol.load_factor(S + V.TB, V.TST, i, k, true);
+    __syncthreads();
+    const double y = i < k ? Trow.dot(S + V.VV, k) : 0.0;
+    S[V.LV + i] = y;
+    __syncthreads();
+    const double lam = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
+    const double lmx = imax<64>(i < k ? fabs(lam) : 0.0);
+    const double neg = imax<64>((i < k && !w.aeq) ? -lam : 0.0);
+    if (!(-imax<64>(-piv) > 1e-12) || neg > 1e-12 * (1.0 + lmx)) {
+        Trow.zero_from(0);
+        Tcol.zero_from(0);
+        __syncthreads();
+        return false;
+    }
+    w.lam = (i < k && !w.aeq) ? fmax(lam, 0.0) : lam;
+    S[V.RV + i] = i < k ? w.sgn * w.lam : 0.0;
+    __syncthreads();
+    // activities move by Gamma[:, A] (sgn lambda); lane j keeps Gamma[j][act_q] for the loop
+#pragma unroll
+    for (int q = 0; q < KM; ++q) {
+        const int aq = __shfl(w.act, q < k ? q : 0);
+        GA.put(q, kind != 0 && q < k, kind != 0 ? pb.gamma(i, aq) : 0.0);
+    }
+    if (kind != 0) s_i += GA.dot(S + V.RV, k);
+    w.onact = slot >= 0;
+    w.k = k;
+    w.iters = 1;
+    g = w;
+    __syncthreads();
+    return true;
+}
+
+// The side (+1 lower, -1 upper; 0 inactive or an equality slot) with which this lane's row ended
+// in the active set: what the next solve of the instance warm-starts from. Every lane calls it.
+__device__ __forceinline__ int warm_record(double *S, const GiVecs &V, int i, const GiState &g)
+{
+    S[V.WV + i] = 0.0;
+    __syncthreads();
+    if (i < g.k && !g.aeq) S[V.WV + g.act] = g.sgn;
+    __syncthreads();
+    const double v = S[V.WV + i];
+    __syncthreads();
+    return v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
+}
+
 // The loop itself (lane i = constraint row i; kind 0 disabled, 1 equality already in the
 // active set, 2 a row with limits [lo, hi], lo == hi an equality added when violated).
 // Statuses: 1 step cap, 2 no step exists (the rows are inconsistent: infeasible), 3 the slot

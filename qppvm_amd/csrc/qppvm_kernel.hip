@@ -305,8 +305,8 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         const int n = a.n;
         const bool row = valid && i < n;
         const double h_i = row ? a.h[b * n + i] : 0.0;
-        const double lo = row ? a.tau_min[i] - h_i : -kInf;
-        const double hi = row ? a.tau_max[i] - h_i : kInf;
+        double lo = -kInf, hi = kInf;
+        if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
         const double *qs = a.q1_scr + b * kM0Max * NP;
         __syncthreads(); // the previous instance's LDS is dead
 #pragma unroll
@@ -368,8 +368,9 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     const bool row = rep && i < n;
     const double h_i = row ? a.h[b * n + i] : 0.0;
     const bool warm = rep && a.ws_hint[b] != 0;
-    const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, rep, row ? a.tau_min[i] - h_i : -kInf,
-                                               row ? a.tau_max[i] - h_i : kInf, warm);
+    double lo = -kInf, hi = kInf;
+    if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
+    const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, rep, lo, hi, warm);
     WBQ_STAMP(11);
     int status = ro.status, iters = 0;
     bool infeasible = false;
@@ -664,10 +665,12 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     double x_i = tau_imp_i; // x = M u = tau_imp + M G^T c
 #pragma unroll
     for (int c = 0; c < M0; ++c) x_i = fma(Y[c], cv[c], x_i);
-    const double lo = row ? a.tau_min[ic] - h_i : -kInf;
-    const double hi = row ? a.tau_max[ic] - h_i : kInf;
+    double lo = -kInf, hi = kInf;
+    if (row) torque_box(a, ic, q_i, qd_i, h_i, lo, hi);
     int status = 0;
     if (a.limits_crossed) status = 2; // tau_min > tau_max somewhere: infeasible everywhere
+    // the JointLimits box can empty per instance (a joint beyond its limit and moving outwards)
+    if (a.joint_limits && imax<NP>((row && lo > hi) ? 1.0 : 0.0) > 0.0) status = 2;
     if (notspd) status = 3;           // (instance-uniform: pivots are broadcast values)
     // rows dropped as dependent are not met: y* != b0, level 0 itself is infeasible at b0 and
     // the active-set kernel runs the level-0 repair (BVLS for y*) first

@@ -281,8 +281,11 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         const int j = ci - m0;
         kind = 2;
         const double hj = a.h[b * n + j];
-        lo = R ? R[RepairIn::LO + j] : a.tau_min[j] - hj;
-        hi = R ? R[RepairIn::HI + j] : a.tau_max[j] - hj;
+        torque_box(a, j, a.q[b * n + j], a.qd[b * n + j], hj, lo, hi);
+        if (R) {
+            lo = R[RepairIn::LO + j];
+            hi = R[RepairIn::HI + j];
+        }
         s_i = S[L.X0 + j];
     }
     __syncthreads();
@@ -298,9 +301,18 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     Trow.zero_from(0);
     S[L.DUM + i] = 0.0;
     GiState gs;
-    gs.status = st0 != 0 ? st0 : (notspd ? 3 : (a.limits_crossed ? 2 : 0));
+    // the JointLimits box can empty per instance (a joint beyond its limit and moving outwards)
+    const bool empty_box = a.joint_limits && __any(kind == 2 && ci >= m0 && lo > hi);
+    gs.status = st0 != 0 ? st0 : (notspd ? 3 : ((a.limits_crossed || empty_box) ? 2 : 0));
     __syncthreads();
-    if (gs.status == 0) {
+    const W1mGi pb{S, &L, m0, n, i, n};
+    const GiVecs gv{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS};
+    bool warm = false;
+    if (gs.status == 0 && !R && a.ws_rows) { // level-0 rows + the last solve's active bounds in one batch
+        const int wsg = (ci >= m0 && kind == 2) ? (int)a.ws_rows[b * 64 + i] : 0;
+        warm = warm_start<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, kind == 2 && ci < m0, wsg);
+    }
+    if (gs.status == 0 && !warm) {
         // The m0 level-0 rows in one batch when Gamma_EE is well conditioned (dependent rows
         // are left to the loop, which never adds them): lane r < m0 holds row r of Gamma_EE, a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane c
@@ -363,14 +375,10 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
             __syncthreads();
         }
     }
-    {
-        const W1mGi pb{S, &L, m0, n, i, n};
-        dual_gi<64>(pb, S, GiVecs{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS}, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs,
-                    a.max_iter);
-    }
+    dual_gi<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs, a.max_iter);
     __syncthreads();
     int status = gs.status;
-    if ((status == 2 || status == 3) && !R && !a.limits_crossed && !notspd) {
+    if ((status == 2 || status == 3) && !R && !a.limits_crossed && !empty_box && !notspd) {
         // no step: level 0 is not attainable at b0 inside the limits; or the active set went
         // numerically dependent, which near-inconsistent level-0 rows also cause -> repair
         // kernel (y* and the pins make the level-1 rows consistent)
@@ -399,6 +407,10 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
             u = fma(w, c < m0 ? S[L.XG + c * L.QS + (i < NQ ? i : 0)] : (c - m0 == i ? 1.0 : 0.0), u);
         }
         rollout_step(a, b, i, row, u, status == 0);
+    }
+    if (a.ws_rows) { // the next solve's warm start (a repaired solve's pinned problem: cold then)
+        const int wrec = warm_record(S, gv, i, gs);
+        a.ws_rows[b * 64 + i] = (signed char)((status == 0 && !R && kind == 2 && ci >= m0) ? wrec : 0);
     }
     if (i == 0) {
         a.status[b] = status;
@@ -436,8 +448,9 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
         const int ic = row ? i : n - 1;
         const double h_i = row ? a.h[b * n + i] : 0.0;
         __syncthreads(); // the previous instance's LDS is dead
-        const RepairOut ro = level0_repair<64, M0>(a, 0, b, i, true, row ? a.tau_min[i] - h_i : -kInf,
-                                                   row ? a.tau_max[i] - h_i : kInf, false);
+        double lo = -kInf, hi = kInf;
+        if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
+        const RepairOut ro = level0_repair<64, M0>(a, 0, b, i, true, lo, hi, false);
         if (ro.unique && !a.integrate) { // level 1 over a single feasible point: x = x* (wave-uniform)
             int status = ro.status;
             double tau_i = row ? ro.x + h_i : h_i;

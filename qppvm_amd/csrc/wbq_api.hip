@@ -70,6 +70,8 @@ struct wbq_ctx {
     int *wl = nullptr;   // [2][max_batch] work lists
     unsigned char *ws_hint = nullptr; // [B] warm start (see wbq_kernels.h)
     signed char *ws_state = nullptr;  // [B][NP]
+    signed char *ws_rows = nullptr;   // [B][64] final active set per instance (contact, W1 = M)
+    double *jl = nullptr;             // [4][n] joint-limit box: q_min, q_max, Kjl, Djl (JointLimits toggle)
     size_t np = 0;
     int epoch = 0;
 };
@@ -199,6 +201,7 @@ int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare)
     a.wl = c->wl;
     a.epoch = c->epoch;
     a.prepare = prepare ? 1 : 0;
+    a.ws_rows = c->ws_rows;
     WBQ_HIP(hipSetDevice(c->device));
     if (prepare) {
         WBQ_HIP(wbq::launch_contact(a, c->stream, nullptr));
@@ -236,6 +239,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     if (d.select_mode != WBQ_SELECT_SUBTASK && d.select_mode != WBQ_SELECT_TASK) return WBQ_E_INVALID;
     if (d.joint_weight != WBQ_WEIGHT_IDENTITY && d.joint_weight != WBQ_WEIGHT_INERTIA) return WBQ_E_INVALID;
     if (!d.Kc || !d.Dc || !d.Kq || !d.Dq || !d.tau_max || !d.tau_min) return WBQ_E_INVALID;
+    if (d.joint_limits && (!d.q_min || !d.q_max || !d.Kjl || !d.Djl)) return WBQ_E_INVALID;
     int m0 = 0;
     int sel[wbq::kM0Max];
     for (int t = 0; t < d.ntasks; ++t) {
@@ -251,6 +255,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     wbq_ctx *c = new wbq_ctx();
     c->d = d;
     c->d.Kc = c->d.Dc = c->d.Kq = c->d.Dq = c->d.tau_max = c->d.tau_min = nullptr;
+    c->d.q_min = c->d.q_max = c->d.Kjl = c->d.Djl = nullptr;
+    c->d.joint_limits = d.joint_limits ? 1 : 0;
     if (c->d.max_iter <= 0) c->d.max_iter = 4 * d.n + 32;
     c->m0 = m0;
     c->device = device;
@@ -268,6 +274,11 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
               hipMalloc(&c->Kq, n * 8) == hipSuccess && hipMalloc(&c->Dq, n * 8) == hipSuccess &&
               hipMalloc(&c->tmax, n * 8) == hipSuccess && hipMalloc(&c->tmin, n * 8) == hipSuccess &&
               hipMalloc(&c->row_sel, sizeof(int) * wbq::kM0Max) == hipSuccess;
+    if (ok && d.joint_limits) // [q_min | q_max | Kjl | Djl]
+        ok = hipMalloc(&c->jl, 4 * n * 8) == hipSuccess && hipMemcpy(c->jl, d.q_min, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(c->jl + n, d.q_max, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(c->jl + 2 * n, d.Kjl, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(c->jl + 3 * n, d.Djl, n * 8, hipMemcpyHostToDevice) == hipSuccess;
     c->nfield = 8;
     for (int f = 0; f < 8; ++f) c->fe[f] = field_elems(d, f);
     size_t in_elems = 0;
@@ -298,6 +309,8 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
              hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
              hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
+        if (ok && d.joint_weight == WBQ_WEIGHT_INERTIA) // the dual loop's warm start (dual_gi.h)
+            ok = hipMalloc(&c->ws_rows, B * 64) == hipSuccess && hipMemset(c->ws_rows, 0, B * 64) == hipSuccess;
         c->np = np;
         if (!ok) return cleanup(WBQ_E_DEVICE);
     }
@@ -364,6 +377,7 @@ int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
               hipMalloc(&c->dev_x, B * c->nx * 8) == hipSuccess &&
               hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
               hipMalloc(&c->wl, B * sizeof(int)) == hipSuccess &&
+              hipMalloc(&c->ws_rows, B * 64) == hipSuccess && hipMemset(c->ws_rows, 0, B * 64) == hipSuccess &&
               hipEventCreateWithFlags(&c->in_copied, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
     ok = hipMemcpy(c->tmax, tmx.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
@@ -535,6 +549,14 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.epoch = c->epoch;
     a.ws_hint = c->ws_hint;
     a.ws_state = c->ws_state;
+    a.ws_rows = c->ws_rows;
+    a.joint_limits = c->d.joint_limits;
+    if (c->jl) {
+        a.q_min = c->jl;
+        a.q_max = c->jl + c->d.n;
+        a.Kjl = c->jl + 2 * c->d.n;
+        a.Djl = c->jl + 3 * c->d.n;
+    }
     a.integrate = integrate;
     a.dt = dt;
     a.prepare = prepare ? 1 : 0;
@@ -679,10 +701,10 @@ int wbq_get_device_outputs(wbq_ctx *c, const double **tau, const int32_t **statu
 
 int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
 {
-    // Drops the per-instance warm start (repair hint + BVLS bound state), stream-ordered
-    // with the solves; a cold instance takes the default path next time.
+    // Drops the per-instance warm start (repair hint, BVLS bound state, the dual loop's last
+    // active set), stream-ordered with the solves; a cold instance takes the default path next time.
     if (!c) return WBQ_E_INVALID;
-    if (!c->ws_hint) return WBQ_SUCCESS; // no warm-start state in this form
+    if (!c->ws_hint && !c->ws_rows) return WBQ_SUCCESS; // no warm-start state in this form
     WBQ_HIP(hipSetDevice(c->device));
     const int B = mask ? c->batch : c->d.max_batch; // a mask has one entry per instance of the batch
     int b = 0;
@@ -693,8 +715,11 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
         }
         int e = b + 1;
         while (e < B && (!mask || mask[e])) ++e;
-        WBQ_HIP(hipMemsetAsync(c->ws_hint + b, 0, (size_t)(e - b), c->stream));
-        WBQ_HIP(hipMemsetAsync(c->ws_state + (size_t)b * c->np, 0, (size_t)(e - b) * c->np, c->stream));
+        if (c->ws_hint) {
+            WBQ_HIP(hipMemsetAsync(c->ws_hint + b, 0, (size_t)(e - b), c->stream));
+            WBQ_HIP(hipMemsetAsync(c->ws_state + (size_t)b * c->np, 0, (size_t)(e - b) * c->np, c->stream));
+        }
+        if (c->ws_rows) WBQ_HIP(hipMemsetAsync(c->ws_rows + (size_t)b * 64, 0, (size_t)(e - b) * 64, c->stream));
         b = e;
     }
     return WBQ_SUCCESS;
@@ -795,6 +820,8 @@ void wbq_destroy(wbq_ctx *c)
     if (c->wl) (void)hipFree(c->wl);
     if (c->ws_hint) (void)hipFree(c->ws_hint);
     if (c->ws_state) (void)hipFree(c->ws_state);
+    if (c->ws_rows) (void)hipFree(c->ws_rows);
+    if (c->jl) (void)hipFree(c->jl);
     if (c->dev_x) (void)hipFree(c->dev_x);
 
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -873,6 +900,8 @@ int prime_contact(wbq_ctx *c)
     int rc = wbq_set_contact_inputs(c, &in);
     if (rc == WBQ_SUCCESS) rc = solve_impl(c, 0, 0.0, true);
     if (rc == WBQ_SUCCESS) rc = wbq_solve(c);
+    if (rc == WBQ_SUCCESS) rc = wbq_sync(c);
+    if (rc == WBQ_SUCCESS) rc = wbq_reset_warmstart(c, nullptr);
     if (rc == WBQ_SUCCESS) rc = wbq_sync(c);
     prime_reset(c);
     return rc;

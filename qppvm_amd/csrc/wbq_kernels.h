@@ -47,6 +47,13 @@ struct QppvmArgs {
     // directly; state = BVLS bound state (-1/0/+1 per joint) of that repair
     unsigned char *ws_hint; // [B]
     signed char *ws_state;  // [B][NP]
+    // W1 = M: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last solve's
+    // final active set, per instance ([B][64]; dual_gi.h warm_start)
+    signed char *ws_rows;
+    // JointLimits toggle (include/wbq.h): the box also holds Kjl (q_min - q) - Djl qd <= tau <=
+    // Kjl (q_max - q) - Djl qd ([n] each, device)
+    int joint_limits;
+    const double *q_min, *q_max, *Kjl, *Djl;
     // MPC rollout step (wbq_rollout): after the final tau of an instance, qdd = M^-1 (tau - h)
     // and semi-implicit Euler on q, qd in place
     int integrate;
@@ -56,6 +63,21 @@ struct QppvmArgs {
     // lock and never allocates (include/wbq.h: wbq_solve is RT-safe)
     int prepare;
 };
+
+// The box on x = tau - h of joint j (QPPVMPlugin.cpp:203-205: tau limits shifted by -h; with the
+// JointLimits toggle also the joint-limit barrier at the joint's q, qd). lo > hi: the instance is
+// infeasible (status 2).
+__device__ __forceinline__ void torque_box(const QppvmArgs &a, int j, double q, double qd, double h, double &lo,
+                                           double &hi)
+{
+    double l = a.tau_min[j], u = a.tau_max[j];
+    if (a.joint_limits) {
+        l = fmax(l, a.Kjl[j] * (a.q_min[j] - q) - a.Djl[j] * qd);
+        u = fmin(u, a.Kjl[j] * (a.q_max[j] - q) - a.Djl[j] * qd);
+    }
+    lo = l - h;
+    hi = u - h;
+}
 
 constexpr int kStamps = 20; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12
 
@@ -104,6 +126,9 @@ struct ContactArgs {
     int *wl;         // [B]
     int epoch;
     int prepare;     // as QppvmArgs::prepare
+    // warm start: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last
+    // solve's final active set, per instance ([B][64]; dual_gi.h warm_start)
+    signed char *ws_rows;
 };
 
 // Semi-implicit Euler of one joint of instance b in place (lane i owns joint i of its

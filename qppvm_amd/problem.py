@@ -65,6 +65,13 @@ class QPPVMProblem:
     tau_max: np.ndarray | float = 150.0
     tau_min: np.ndarray | float | None = None
     max_iter: int = 0  # 0 = default cap (4 n + 32 active-set steps)
+    # JointLimits toggle (QPPVMPlugin.cpp:169-171, commented out of the reference stack): the box
+    # also holds Kjl (q_min - q) - Djl qd <= tau <= Kjl (q_max - q) - Djl qd (include/wbq.h)
+    joint_limits: bool = False
+    q_min: np.ndarray | float = -np.pi
+    q_max: np.ndarray | float = np.pi
+    Kjl: np.ndarray | float = 50.0
+    Djl: np.ndarray | float = 20.0
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -88,6 +95,9 @@ class QPPVMProblem:
         self.Dq = _vec(self.Dq, n, "Dq")
         self.tau_max = _vec(self.tau_max, n, "tau_max")
         self.tau_min = -self.tau_max if self.tau_min is None else _vec(self.tau_min, n, "tau_min")
+        self.joint_limits = bool(self.joint_limits)
+        for k in ("q_min", "q_max", "Kjl", "Djl"):
+            setattr(self, k, _vec(getattr(self, k), n, k))
         if self.select_mode not in (SELECT_SUBTASK, SELECT_TASK):
             raise ValueError("select_mode must be SELECT_SUBTASK or SELECT_TASK")
         if self.joint_weight not in (WEIGHT_IDENTITY, WEIGHT_INERTIA):

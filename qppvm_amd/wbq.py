@@ -40,7 +40,9 @@ class Desc(ctypes.Structure):
                 ("joint_weight", ctypes.c_int), ("max_batch", ctypes.c_int),
                 ("max_iter", ctypes.c_int),
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
-                ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+                ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
+                ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p)]
 
 
 class Inputs(ctypes.Structure):
@@ -160,6 +162,11 @@ class QPPVMSolver:
         self._keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
                       for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
         d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [_ptr(a) for a in self._keep]
+        if prob.joint_limits:
+            jl = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64) for k in ("q_min", "q_max", "Kjl", "Djl")]
+            self._keep += jl
+            d.joint_limits = 1
+            d.q_min, d.q_max, d.Kjl, d.Djl = [_ptr(a) for a in jl]
         h = ctypes.c_void_p()
         rc = self.lib.wbq_create(ctypes.byref(d), int(device), ctypes.byref(h))
         if rc != SUCCESS:

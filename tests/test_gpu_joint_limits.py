@@ -1,0 +1,65 @@
+"""GPU: the JointLimits toggle (QPPVMPlugin.cpp:169-171, commented out of the reference stack;
+include/wbq.h wbq_desc.joint_limits). Every instance's box on tau also holds the joint-limit
+barrier Kjl (q_min - q) - Djl qd <= tau <= Kjl (q_max - q) - Djl qd, so the box varies per
+instance and can empty (status 2). GPU (fast kernel n <= 32, the n > 32 active-set kernel, W1 =
+M) against the oracle (oracle/wbq_oracle.c:wbq_ref_assemble): statuses equal, tau within 1e-6."""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from qppvm_amd.problem import QPPVMProblem
+from qppvm_amd.synth import qppvm_instances
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def wbq_mod():
+    from qppvm_amd import build, wbq
+    build.build()
+    return wbq
+
+
+def solve(wbq_mod, prob, inp):
+    s = wbq_mod.QPPVMSolver(prob, max_batch=inp["h"].shape[0])
+    try:
+        return s.solve_batch(inp)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("n,weight", [(30, 0), (39, 0), (30, 1)])
+def test_joint_limits_match_oracle(wbq_mod, oracle_lib, n, weight):
+    inp = qppvm_instances(QPPVMProblem(n=n), 128, seed=200 + n)
+    # ~20 % of the joint-limit bounds active (the synthetic torques are O(1e3-1e4))
+    prob = QPPVMProblem(n=n, tau_max=1e6, joint_weight=weight, joint_limits=True, q_min=-3.0, q_max=3.0,
+                        Kjl=3000.0, Djl=300.0)
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+    tau, st, it = solve(wbq_mod, prob, inp)
+    np.testing.assert_array_equal(st, st_r)
+    ok = st == 0
+    assert ok.mean() > 0.9
+    assert rel_err(tau[ok], tau_r[ok]) <= TOL, rel_err(tau[ok], tau_r[ok])
+    q, qd = inp["q"], inp["qd"]
+    hi = np.minimum(prob.tau_max, 3000.0 * (3.0 - q) - 300.0 * qd)
+    lo = np.maximum(prob.tau_min, 3000.0 * (-3.0 - q) - 300.0 * qd)
+    act = (np.abs(tau - lo) < 1e-7 * (1 + np.abs(lo))) | (np.abs(tau - hi) < 1e-7 * (1 + np.abs(hi)))
+    assert act[ok].mean() > 0.1  # the joint-limit bounds really bind
+    assert np.all(tau[ok] <= hi[ok] + 1e-7 * (1 + np.abs(hi[ok])))
+    assert np.all(tau[ok] >= lo[ok] - 1e-7 * (1 + np.abs(lo[ok])))
+
+
+def test_joint_limits_empty_box_is_infeasible(wbq_mod, oracle_lib):
+    """A joint far beyond its upper limit and moving outwards: the barrier asks for more torque
+    than the effort limit allows -- no feasible tau, status 2 and tau = h on both sides."""
+    n = 30
+    inp = qppvm_instances(QPPVMProblem(n=n), 16, seed=7)
+    inp["q"][::2, 3] = 3.1
+    inp["qd"][::2, 3] = 5.0
+    prob = QPPVMProblem(n=n, tau_max=150.0, joint_limits=True, q_min=-1.0, q_max=1.0, Kjl=100.0, Djl=20.0)
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+    tau, st, _ = solve(wbq_mod, prob, inp)
+    np.testing.assert_array_equal(st, st_r)
+    assert np.all(st[::2] == 2)
+    np.testing.assert_array_equal(tau[st != 0], inp["h"][st != 0])
