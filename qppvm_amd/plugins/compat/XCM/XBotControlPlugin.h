@@ -361,6 +361,13 @@ public:
     virtual bool getPose(const std::string &link, Eigen::Affine3d &w_T_link) const = 0;
     virtual bool getJacobian(const std::string &link, Eigen::MatrixXd &J) const = 0;
     virtual bool getInertiaMatrix(Eigen::MatrixXd &M) const = 0;
+    // joint position limits (QPPVMPlugin.cpp:120: the JointLimits constraint's input)
+    virtual bool getJointLimits(Eigen::VectorXd &q_min, Eigen::VectorXd &q_max) const
+    {
+        q_min.setConstant(getJointNum(), -3.14159265358979);
+        q_max.setConstant(getJointNum(), 3.14159265358979);
+        return true;
+    }
     // XBotInterface computeJdotQdot(link, point, jdotqdot) / getPointPosition(link, point, p): the
     // bias acceleration and the position of a point given in the link frame (ForceAcc.cpp:164)
     virtual bool computeJdotQdot(const std::string &link, const Eigen::Vector3d &point, Eigen::Vector6d &jdqd) const

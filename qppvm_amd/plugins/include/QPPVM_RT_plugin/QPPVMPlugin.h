@@ -37,6 +37,11 @@ public:
     // the dummy driver sets them before init_control_plugin / on_start
     void set_log_prefix(const std::string &prefix) { _log_prefix = prefix; }
     void set_reference_trajectory(bool on) { _set_ref = on; }
+    // the JointLimits constraint the reference builds and comments out of its stack (:169-173):
+    // set before init_control_plugin
+    void set_joint_limits(bool on) { _use_joint_limits = on; }
+    const Eigen::VectorXd &joint_limit(int which) const { return which ? _q_max : _q_min; }
+    const Eigen::VectorXd &joint_limit_gain(int which) const { return which ? _d_jl : _k_jl; }
     // the Cartesian references the tasks track (t = 0 right, 1 left): the on_start poses, the
     // left one replaced by the _set_ref sinusoid
     const Eigen::Affine3d &ee_reference(int t) const { return _ee_ref[t]; }
@@ -64,6 +69,8 @@ private:
     // _set_ref: left end-effector reference on a circle in the y-z plane (:217-223), on the
     // reference's KDL frames (QPPVMPlugin.h:98-99)
     bool _set_ref = false;
+    bool _use_joint_limits = false;
+    Eigen::VectorXd _q_min, _q_max, _k_jl, _d_jl;
     KDL::Frame _start_pose;
     KDL::Frame _ref;
     std::string _log_prefix = "/tmp/qppvm_log";

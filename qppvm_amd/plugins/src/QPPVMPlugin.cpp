@@ -80,6 +80,19 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle) // :42-199
     d.Dq = Dq.data();
     d.tau_max = _tau_max_const.data();
     d.tau_min = _tau_min_const.data();
+    if (_use_joint_limits) { // :120-126 and :169-171 (commented out in the reference)
+        _model->getJointLimits(_q_min, _q_max);
+        Eigen::VectorXd q_range = _q_max - _q_min;
+        _q_max -= q_range * 0.1;
+        _q_min += q_range * 0.1;
+        _k_jl = k0 * 10; // _joint_limits->setGains(k0*10, d0*20)
+        _d_jl = d0 * 20;
+        d.joint_limits = 1;
+        d.q_min = _q_min.data();
+        d.q_max = _q_max.data();
+        d.Kjl = _k_jl.data();
+        d.Djl = _d_jl.data();
+    }
     const int rc = wbq_create(&d, 0, &_ctx);
     if (rc != WBQ_SUCCESS) {
         std::fprintf(stderr, "QPPVMPlugin: wbq_create failed (%d)\n", rc);

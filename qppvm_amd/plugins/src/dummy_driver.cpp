@@ -95,7 +95,7 @@ int main(int argc, char **argv)
 {
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
-    bool forceacc = false, stress = false, set_ref = false;
+    bool forceacc = false, stress = false, set_ref = false, joint_limits = false;
     const char *log_prefix = nullptr;
     for (int k = 1; k < argc; ++k) {
         if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
@@ -103,6 +103,7 @@ int main(int argc, char **argv)
         else if (!std::strcmp(argv[k], "--plugin") && k + 1 < argc) forceacc = !std::strcmp(argv[++k], "forceacc");
         else if (!std::strcmp(argv[k], "--stress")) stress = true;
         else if (!std::strcmp(argv[k], "--set-ref")) set_ref = true; // QPPVMPlugin.cpp:217-223
+        else if (!std::strcmp(argv[k], "--joint-limits")) joint_limits = true; // :169-171
         else if (!std::strcmp(argv[k], "--log") && k + 1 < argc) log_prefix = argv[++k];
         else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
             dump = argv[++k];
@@ -119,6 +120,7 @@ int main(int argc, char **argv)
     demo::QPPVMPlugin plugin;
     if (log_prefix) plugin.set_log_prefix(log_prefix);
     plugin.set_reference_trajectory(set_ref);
+    plugin.set_joint_limits(joint_limits);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;

@@ -93,6 +93,12 @@ public:
         return true;
     }
     bool getEffortLimits(Eigen::VectorXd &tmax) const override { tmax.setConstant(n_, 150.0); return true; }
+    bool getJointLimits(Eigen::VectorXd &qmin, Eigen::VectorXd &qmax) const override
+    {
+        qmin.setConstant(n_, -0.3); // the dummy plant starts at q = 0 and moves by a few 0.1 rad
+        qmax.setConstant(n_, 0.3);
+        return true;
+    }
     bool getRobotState(const std::string &, Eigen::VectorXd &q) const override { q.setZero(n_); return true; }
     bool setJointPosition(const Eigen::VectorXd &q) override { for (int j = 0; j < n_; ++j) q_[j] = q[j]; return true; }
     bool setJointVelocity(const Eigen::VectorXd &qd) override { for (int j = 0; j < n_; ++j) qd_[j] = qd[j]; return true; }

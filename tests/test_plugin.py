@@ -61,6 +61,29 @@ def test_dummy_driver_matches_oracle(tmp_path, oracle_lib, plant):
     assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, rel_err(d["tau"][ok], tau_r[ok])
 
 
+def test_dummy_driver_joint_limits(tmp_path, oracle_lib):
+    """The JointLimits toggle of the QPPVM shell (QPPVMPlugin.cpp:120-126, 169-171: limits from
+    ModelInterface::getJointLimits shrunk by 10 % of the range, gains k0*10, d0*20): every dumped
+    tick re-solved by the oracle with the same joint-limit box (dummy plant: limits +-0.3 rad,
+    robot stiffness 500, damping 10)."""
+    from qppvm_amd import build
+    driver = build.build_plugins()[1]
+    dump = str(tmp_path / "dump.bin")
+    r = subprocess.run([driver, "--ticks", "300", "--dump", dump, "60", "--joint-limits"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, d = read_dump(dump)
+    prob = QPPVMProblem(n=n, tau_max=150.0, joint_limits=True, q_min=-0.24, q_max=0.24, Kjl=5000.0, Djl=200.0)
+    inp = {k: np.ascontiguousarray(d[k]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+    np.testing.assert_array_equal(d["status"], st_r)
+    ok = st_r == 0
+    assert ok.sum() >= len(ok) - 2
+    assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, rel_err(d["tau"][ok], tau_r[ok])
+    hi = np.minimum(150.0, 5000.0 * (0.24 - d["q"]) - 200.0 * d["qd"])
+    assert np.any(np.abs(d["tau"][ok] - hi[ok]) < 1e-6 * (1 + np.abs(hi[ok])))  # the joint-limit box binds
+
+
 def read_forceacc_dump(path):
     raw = open(path, "rb").read()
     n, nc, ticks = (int(v) for v in np.frombuffer(raw[:12], dtype=np.int32))
