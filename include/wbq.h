@@ -120,13 +120,14 @@ typedef struct {
     const double *M, *J, *pose, *pose_ref, *q, *qd, *qref, *h;
 } wbq_inputs;
 
-/* Contact form: x = [qdd (n); f_c (3 per contact)] (ForceAcc.cpp:58-72); level 0 = waist
+/* Contact form: x = [qdd (n); w_c (wrench_dim per contact)] (ForceAcc.cpp:58-72); level 0 = waist
  * acceleration task, level 1 = postural + feet acceleration tasks + eps_f ||f||^2 (the explicit
  * minimum-norm tie-break of the internal forces); both levels: dynamic feasibility on the 6
  * floating-base rows, force box for active contacts (f = 0 for inactive ones), optional
  * actuated torque rows tau_min <= M_a qdd + h_a - J_c,a^T f <= tau_max. */
 typedef struct {
-    int n;            /* DoF incl. the floating base (first n_fb coordinates); n + 6 + 3 nc <= 64 */
+    int n;            /* DoF incl. the floating base (first n_fb coordinates); n + wd nc <= 64 and the
+                       * constraint rows (6 or n) + 6 + wd nc (+ 4 nc with mu) <= 64 */
     int n_fb;         /* must be 6 */
     int nc;           /* contacts, 1..4 */
     int torque_rows;  /* 0/1 */
@@ -136,6 +137,13 @@ typedef struct {
     double f_lb[3], f_ub[3];                   /* force box (reference: -1000,-1000,10 / 1000) */
     double eps_f;                              /* > 0 */
     const double *tau_max, *tau_min;           /* [n] (used with torque_rows) */
+    /* SURVEY.md 8f-2 options; a zero-initialised tail is the reference's stack */
+    int wrench_dim;            /* 3 (0 = 3): w_c = [f_c; 0]; 6: x carries the full wrench w_c = [f_c; m_c]
+                                * ("put 6 for full wrench", ForceAcc.cpp:67), boxed by [f_lb, m_lb] ..
+                                * [f_ub, m_ub] (:74-76), J_c^T w_c over all six Jacobian rows */
+    double m_lb[3], m_ub[3];   /* moment box of a 6-D wrench (reference -1 / 1) */
+    double mu;                 /* > 0: linearised friction pyramid |f_x| <= mu f_z, |f_y| <= mu f_z per
+                                * active contact (world frame, 4 rows); 0: none (the reference) */
 } wbq_contact_desc;
 
 /* Contact-form batch, fp64 row-major, instance-major:
@@ -174,7 +182,7 @@ int wbq_set_state(wbq_ctx *ctx, const double *q, const double *qd, int memory);
 int wbq_sync(wbq_ctx *ctx);
 /* Synchronous copy of the last solve's outputs to host memory (any pointer may be NULL). */
 int wbq_get_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
-/* Contact form: synchronous copy of the last solve's x = [qdd; f] ([batch][n + 3 nc]). */
+/* Contact form: synchronous copy of the last solve's x = [qdd; w] ([batch][n + wrench_dim nc]). */
 int wbq_get_contact_outputs(wbq_ctx *ctx, double *x);
 /* Write outputs into caller-owned device buffers ([batch][n] / [batch]) instead of the
  * context's (any NULL pointer reverts that output to the context buffer). */

@@ -176,7 +176,9 @@ class _CDesc(ctypes.Structure):
                 ("Kp_w", ctypes.c_double), ("Kd_w", ctypes.c_double), ("Kp_f", ctypes.c_double),
                 ("Kd_f", ctypes.c_double), ("Kp_p", ctypes.c_double), ("Kd_p", ctypes.c_double),
                 ("f_lb", ctypes.c_double * 3), ("f_ub", ctypes.c_double * 3), ("eps_f", ctypes.c_double),
-                ("torque_rows", ctypes.c_int), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+                ("torque_rows", ctypes.c_int), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
+                ("wrench_dim", ctypes.c_int), ("m_lb", ctypes.c_double * 3), ("m_ub", ctypes.c_double * 3),
+                ("mu", ctypes.c_double)]
 
 
 class _CInst(ctypes.Structure):
@@ -196,6 +198,9 @@ def _cdesc(prob):
         setattr(d, k, float(getattr(prob, k)))
     for k in range(3):
         d.f_lb[k], d.f_ub[k] = prob.f_lb[k], prob.f_ub[k]
+        d.m_lb[k], d.m_ub[k] = prob.m_lb[k], prob.m_ub[k]
+    d.wrench_dim = int(getattr(prob, "wrench_dim", 3))
+    d.mu = float(getattr(prob, "mu", 0.0))
     d.torque_rows = int(bool(prob.torque_rows))
     keep = [np.ascontiguousarray(prob.tau_max, dtype=np.float64), np.ascontiguousarray(prob.tau_min, dtype=np.float64)]
     d.tau_max, d.tau_min = keep[0].ctypes.data, keep[1].ctypes.data
@@ -227,7 +232,7 @@ def contact_assemble(prob, inputs, b=0):
     d, keep = _cdesc(prob)
     s, arrs = _cinst(inputs, b)
     nx = prob.nx
-    mi = 3 * prob.nc + (prob.n - prob.n_fb if prob.torque_rows else 0)
+    mi = (prob.wrench_dim + (4 if prob.mu > 0 else 0)) * prob.nc + (prob.n - prob.n_fb if prob.torque_rows else 0)
     H, g, E, e = np.zeros((nx, nx)), np.zeros(nx), np.zeros((12, nx)), np.zeros(12)
     C, clo, chi, bw = np.zeros((max(mi, 1), nx)), np.zeros(max(mi, 1)), np.zeros(max(mi, 1)), np.zeros(6)
     lib().wbq_ref_contact_assemble(ctypes.byref(d), ctypes.byref(s), _p(H), _p(g), _p(E), _p(e), _p(C),

@@ -131,6 +131,12 @@ typedef struct {
     double eps_f;       /* min-norm tie-break weight on the forces */
     int torque_rows;    /* a12 extension: actuated torque-limit rows */
     const double *tau_max, *tau_min; /* [n] (rows n_fb.. used when torque_rows) */
+    /* SURVEY 8f-2 extensions (zero-initialised = the reference's point forces, no cone) */
+    int wrench_dim;     /* 3 (0 = 3): w_c = [f_c; 0]; 6: full wrench [f_c; m_c] ("put 6 for full
+                         * wrench", ForceAcc.cpp:67), box [f_lb, m_lb] <= w_c <= [f_ub, m_ub] (:74-76) */
+    double m_lb[3], m_ub[3]; /* moment box of a 6-D wrench (reference -1 / 1) */
+    double mu;          /* > 0: linearised friction pyramid |f_x| <= mu f_z, |f_y| <= mu f_z (world
+                         * frame, 4 rows per active contact); 0: none (the reference) */
 } wbq_ref_contact_desc;
 
 /* One instance: M [n][n], h, q, qd, qref [n]; waist Jw [6][n], jdqd_w [6] (Jdot qd),
@@ -143,14 +149,17 @@ typedef struct {
     int contact_mask;
 } wbq_ref_contact_instance;
 
+/* wrench components per contact (3 or 6) */
+int wbq_ref_contact_wd(const wbq_ref_contact_desc *d);
+
 /* Dense Goldfarb-Idnani dual active set, KKT re-solved by LU each step:
  *   min 0.5 x^T H x + g^T x  s.t.  E x = e (me rows),  clo <= C x <= chi (mi rows),  H SPD. */
 int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const double *E, const double *e,
                     int mi, const double *C, const double *clo, const double *chi, double *x, int *iters);
 
-/* Level-1 data of the contact form (nx = n + 3 nc): H1, g1, E [12][nx] (waist rows with
- * rhs b_w, then dynamic feasibility), C [mi][nx] with clo/chi; bw [6] the waist target.
- * Returns mi. */
+/* Level-1 data of the contact form (nx = n + wd nc, wd = wrench_dim): H1, g1, E [12][nx] (waist
+ * rows with rhs b_w, then dynamic feasibility), C [mi][nx] with clo/chi (mi = wd nc box rows, then
+ * 4 nc friction rows when mu > 0, then n - n_fb torque rows); bw [6] the waist target. Returns mi. */
 int wbq_ref_contact_assemble(const wbq_ref_contact_desc *d, const wbq_ref_contact_instance *in, double *H1,
                              double *g1, double *E, double *e, double *C, double *clo, double *chi, double *bw);
 

@@ -7,8 +7,9 @@
  * restatement whose answers carry a KKT certificate).
  *
  * Reference anchors (files under /root/reference):
- *   src/ForceAcc.cpp:58-72    decision vector x = [qddot (n); f_c (3) per contact]
- *   src/ForceAcc.cpp:74-95    wrench w_c = [f_c; 0_3], box lb=(-1000,-1000,10,..) ub=(1000,..)
+ *   src/ForceAcc.cpp:58-72    decision vector x = [qddot (n); f_c (3) per contact] (:67 "put 6 for
+ *                             full wrench": wrench_dim = 6, x = [qddot; w_c (6) per contact])
+ *   src/ForceAcc.cpp:74-95    wrench w_c = [f_c; 0_3], box lb=(-1000,-1000,10,-1,-1,-1) ub=(1000,..,1)
  *   src/ForceAcc.cpp:83-89    feet acceleration Cartesian tasks (world frame)
  *   src/ForceAcc.cpp:105-107  postural acceleration task
  *   src/ForceAcc.cpp:109-114  DynamicFeasibility: floating-base rows of M qdd + h = sum J_c^T w_c
@@ -25,7 +26,10 @@
  *             s.t. J_w qdd = y0* (level-0 optimality)
  *   both      dynamic feasibility (6 equality rows), force box (inactive contacts: f = 0),
  *             optional actuated torque rows tau_min <= M_a qdd + h_a - J_{c,a}^T f <= tau_max
- *             (row a12, an extension: the reference ForceAcc has none)
+ *             (row a12, an extension: the reference ForceAcc has none), optional linearised
+ *             friction pyramid |f_x| <= mu f_z, |f_y| <= mu f_z per active contact (SURVEY 8f-2;
+ *             the reference has no cone, ForceAcc.cpp:74-76)
+ * With wrench_dim = 6 every "f" above is the 6-D wrench w_c and J_c^T w_c uses all six Jacobian rows.
  * eps_f is the minimum-norm tie-break on the contact forces: with 3+ contacts the forces
  * have an internal null space no task sees; the reference leaves it to qpOASES' Hessian
  * regularisation, which this makes explicit.
@@ -37,6 +41,11 @@
 #include "wbq_oracle.h"
 
 static double cmaxd(double a, double b) { return a > b ? a : b; }
+
+/* |bound|, 0 for an unbounded side (+-1e300): tolerances scale with finite bounds only */
+static double fin(double v) { return fabs(v) < 1e299 ? fabs(v) : 0.0; }
+
+int wbq_ref_contact_wd(const wbq_ref_contact_desc *d) { return d->wrench_dim == 6 ? 6 : 3; }
 
 /* Solve A x = b (A N x N destroyed, b overwritten), LU with partial pivoting. */
 static int lu(int N, double *A, double *b)
@@ -152,8 +161,8 @@ int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const doubl
                 }
                 nn = sqrt(cmaxd(nn, 1e-300));
                 const double vlo = clo[j] - s, vhi = s - chi[j];
-                const double tl = 1e-10 * cmaxd(1.0, cmaxd(fabs(s), fabs(clo[j])));
-                const double th = 1e-10 * cmaxd(1.0, cmaxd(fabs(s), fabs(chi[j])));
+                const double tl = 1e-10 * cmaxd(1.0, cmaxd(fabs(s), fin(clo[j])));
+                const double th = 1e-10 * cmaxd(1.0, cmaxd(fabs(s), fin(chi[j])));
                 if (vlo > tl && vlo / nn > best) best = vlo / nn, bj = j, bside = 1;
                 if (vhi > th && vhi / nn > best) best = vhi / nn, bj = j, bside = -1;
             }
@@ -238,7 +247,7 @@ int wbq_ref_dual_qp(int n, const double *H, const double *g, int me, const doubl
         for (int j = 0; j < mi && status == WBQ_REF_OK; ++j) {
             double s = 0.0;
             for (int i = 0; i < n; ++i) s += C[(size_t)j * n + i] * x[i];
-            const double sc = 1e-8 * cmaxd(1.0, cmaxd(fabs(s), cmaxd(fabs(clo[j]), fabs(chi[j]))));
+            const double sc = 1e-8 * cmaxd(1.0, cmaxd(fabs(s), cmaxd(fin(clo[j]), fin(chi[j]))));
             if (clo[j] - s > sc || s - chi[j] > sc) status = WBQ_REF_NUMERICAL;
         }
     }
@@ -303,8 +312,9 @@ static void cart_acc_rhs(int n, const double *J, const double *jdqd, const doubl
 int wbq_ref_contact_assemble(const wbq_ref_contact_desc *d, const wbq_ref_contact_instance *in, double *H1,
                              double *g1, double *E, double *e, double *C, double *clo, double *chi, double *bw)
 {
-    const int n = d->n, nc = d->nc, nfb = d->n_fb, nx = n + 3 * nc;
-    const int mi = 3 * nc + (d->torque_rows ? n - nfb : 0);
+    const int n = d->n, nc = d->nc, nfb = d->n_fb, wd = wbq_ref_contact_wd(d), nx = n + wd * nc;
+    const int nfr = d->mu > 0.0 ? 4 * nc : 0;
+    const int mi = wd * nc + nfr + (d->torque_rows ? n - nfb : 0);
     double bc[6];
     memset(H1, 0, sizeof(double) * nx * nx);
     memset(g1, 0, sizeof(double) * nx);
@@ -343,28 +353,41 @@ int wbq_ref_contact_assemble(const wbq_ref_contact_desc *d, const wbq_ref_contac
         double *er = E + (size_t)(6 + r) * nx;
         for (int j = 0; j < n; ++j) er[j] = in->M[r * n + j];
         for (int c = 0; c < nc; ++c)
-            for (int k = 0; k < 3; ++k) er[n + 3 * c + k] = -in->Jc[((size_t)c * 6 + k) * n + r];
+            for (int k = 0; k < wd; ++k) er[n + wd * c + k] = -in->Jc[((size_t)c * 6 + k) * n + r];
         e[6 + r] = -in->h[r];
     }
     /* force box (:74-76,91-95); inactive contacts fixed at zero */
     memset(C, 0, sizeof(double) * (size_t)(mi > 0 ? mi : 1) * nx);
     for (int c = 0; c < nc; ++c) {
         const int on = (in->contact_mask >> c) & 1;
-        for (int k = 0; k < 3; ++k) {
-            const int row = 3 * c + k;
-            C[row * nx + n + 3 * c + k] = 1.0;
-            clo[row] = on ? d->f_lb[k] : 0.0;
-            chi[row] = on ? d->f_ub[k] : 0.0;
+        for (int k = 0; k < wd; ++k) {
+            const int row = wd * c + k;
+            C[row * nx + n + wd * c + k] = 1.0;
+            clo[row] = on ? (k < 3 ? d->f_lb[k] : d->m_lb[k - 3]) : 0.0;
+            chi[row] = on ? (k < 3 ? d->f_ub[k] : d->m_ub[k - 3]) : 0.0;
+        }
+    }
+    /* friction pyramid: s_x f_x - mu f_z <= 0 (faces +x, -x), s_y f_y - mu f_z <= 0 (+y, -y);
+     * an inactive contact's rows are left unbounded (its forces are fixed at zero) */
+    for (int c = 0; c < nfr / 4; ++c) {
+        const int on = (in->contact_mask >> c) & 1;
+        for (int k = 0; k < 4; ++k) {
+            const int row = wd * nc + 4 * c + k;
+            double *cr = C + (size_t)row * nx + n + wd * c;
+            cr[k < 2 ? 0 : 1] = (k & 1) ? -1.0 : 1.0;
+            cr[2] = -d->mu;
+            clo[row] = -1e300;
+            chi[row] = on ? 0.0 : 1e300;
         }
     }
     /* a12: actuated torque rows tau_min - h_a <= M_a qdd - sum_c J_c[0:3, a]^T f_c <= tau_max - h_a */
     if (d->torque_rows)
         for (int a = nfb; a < n; ++a) {
-            const int row = 3 * nc + (a - nfb);
+            const int row = wd * nc + nfr + (a - nfb);
             double *cr = C + (size_t)row * nx;
             for (int j = 0; j < n; ++j) cr[j] = in->M[a * n + j];
             for (int c = 0; c < nc; ++c)
-                for (int k = 0; k < 3; ++k) cr[n + 3 * c + k] = -in->Jc[((size_t)c * 6 + k) * n + a];
+                for (int k = 0; k < wd; ++k) cr[n + wd * c + k] = -in->Jc[((size_t)c * 6 + k) * n + a];
             clo[row] = d->tau_min[a] - in->h[a];
             chi[row] = d->tau_max[a] - in->h[a];
         }
@@ -374,8 +397,8 @@ int wbq_ref_contact_assemble(const wbq_ref_contact_desc *d, const wbq_ref_contac
 int wbq_ref_contact_one(const wbq_ref_contact_desc *d, const wbq_ref_contact_instance *in, double *tau,
                         double *x, int *iters, int *l0_repaired)
 {
-    const int n = d->n, nc = d->nc, nx = n + 3 * nc;
-    const int mi = 3 * nc + (d->torque_rows ? n - d->n_fb : 0);
+    const int n = d->n, nc = d->nc, wd = wbq_ref_contact_wd(d), nx = n + wd * nc;
+    const int mi = wd * nc + (d->mu > 0.0 ? 4 * nc : 0) + (d->torque_rows ? n - d->n_fb : 0);
     level_qp L;
     level_alloc(&L, nx, 12, mi);
     double bw[6];
@@ -424,12 +447,12 @@ int wbq_ref_contact_one(const wbq_ref_contact_desc *d, const wbq_ref_contact_ins
         level_free(&Z);
     }
     if (status == WBQ_REF_OK) {
-        /* ForceAcc.cpp:206-218: tau = M qdd + h - sum_c J_c^T [f_c; 0] */
+        /* ForceAcc.cpp:206-218: tau = M qdd + h - sum_c J_c^T w_c (w_c = [f_c; 0] or the 6-D wrench) */
         for (int i = 0; i < n; ++i) {
             double s = in->h[i];
             for (int j = 0; j < n; ++j) s += in->M[i * n + j] * x[j];
             for (int c = 0; c < nc; ++c)
-                for (int k = 0; k < 3; ++k) s -= in->Jc[((size_t)c * 6 + k) * n + i] * x[n + 3 * c + k];
+                for (int k = 0; k < wd; ++k) s -= in->Jc[((size_t)c * 6 + k) * n + i] * x[n + wd * c + k];
             tau[i] = s;
         }
     } else {
@@ -446,7 +469,7 @@ void wbq_ref_contact_batch(const wbq_ref_contact_desc *d, int B, const double *M
                            const double *pose_c, const double *pose_c_ref, const int32_t *cmask, double *tau,
                            double *x, int32_t *status, int32_t *iters, int32_t *l0_repaired)
 {
-    const int n = d->n, nc = d->nc, nx = n + 3 * nc;
+    const int n = d->n, nc = d->nc, nx = n + wbq_ref_contact_wd(d) * nc;
     for (int b = 0; b < B; ++b) {
         wbq_ref_contact_instance in;
         in.M = M + (size_t)b * n * n;

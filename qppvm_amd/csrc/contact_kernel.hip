@@ -1,14 +1,17 @@
 // contact_kernel.hip -- batched contact-form (ForceAcc) whole-body QP for gfx950 (MI355X), fp64.
 //
-// One instance per wave64 block. The math (SURVEY.md 8a rows a10-a12; reference
+// One instance per wave64 block. The math (SURVEY.md 8a rows a10-a12, 8f-2; reference
 // src/ForceAcc.cpp; the build's written spec is oracle/wbq_oracle_contact.c):
 //   x = [qdd (n); f_c (3) per contact]                                     (:58-72)
+//       (wrench_dim 6: w_c = [f_c; m_c], "put 6 for full wrench" :67; every f_c below is then w_c,
+//        its box [f_lb, m_lb] <= w_c <= [f_ub, m_ub] and J_c^T w_c runs over all six rows)
 //   level 0   min ||J_w qdd - b_w||^2             (waist / pelvis task)       (:118-122)
 //   level 1   min ||qdd - b_p||^2 + sum_c ||J_c qdd - b_c||^2 + eps_f ||f||^2 (:83-89, :105-107)
 //             s.t. J_w qdd = y0* = b_w (level 0 attained, the generic case)
 //   both      M_fb qdd - sum_c J_c[0:3, fb]^T f_c = -h_fb   (DynamicFeasibility, :109-114)
 //             f_lb <= f_c <= f_ub for active contacts, f_c = 0 otherwise  (:74-76, :91-95)
 //             optional actuated torque rows tau_min <= M_a qdd + h_a - J_ca^T f <= tau_max (a12)
+//             optional friction pyramid |f_x| <= mu f_z, |f_y| <= mu f_z per active contact (8f-2)
 //   tau = M qdd + h - sum_c J_c^T [f_c; 0]                                  (:206-218)
 // with Cartesian acceleration tasks J qdd = Kp e - Kd J qd - Jdot qd and the postural task
 // qdd = Kp (q_ref - q) - Kd qd.
@@ -43,27 +46,36 @@
 namespace wbq {
 namespace {
 
-// Grid of the level-0 repair kernel (grid-stride over its work list; a solve with nothing to
-// repair costs one near-empty launch of this many blocks)
+// Largest grid of the level-0 repair kernel (grid-stride over its work list; sized per solve from
+// the counts of the last solves, FollowGrid in wbq_kernels.h)
 constexpr unsigned kContactRepairGrid = 256;
 
-// Per-instance LDS layout in doubles. Compact constraint index ci (= GI lane):
+// Per-instance LDS layout in doubles. Compact constraint index ci (= GI lane), NF = wd nc force
+// variables (3 forces or the 6-D wrench per contact):
 //   ci <  NJ             joint row a = ci (a < 6: dynamic feasibility, an equality;
 //                        a >= 6: actuated torque row, only with torque rows, NJ = n)
 //   NJ <= ci < NJ + 6    waist row r = ci - NJ (equality, target b_w)
-//   NJ + 6 <= ci < ME    force row f = ci - NJ - 6 (box; disabled for inactive contacts)
+//   NJ + 6 <= ci < NB    force row f = ci - NJ - 6 (box; disabled for inactive contacts)
+//   NB <= ci < ME        friction face k = (ci - NB) % 4 of contact (ci - NB) / 4 (with mu > 0):
+//                        s f_x - mu f_z <= 0 (k = 0, 1: s = +-1), s f_y - mu f_z <= 0 (k = 2, 3)
 // X = H^-1 A_q^T has one column ("slot") per q-bearing row, slot = ci, plus x0 at NJ + 6.
 struct ContactLayout {
-    int NJ, NR, ME, NX, QS, FS, GS, TS;
+    int NJ, NR, NF, WD, NB, ME, NX, QS, FS, GS, TS;
+    double MU;
     int AQJ, AQW, FFJ, XT, GM, TT, JC, PN, RH, HR, XV, X0, VV, LV, RV, WV, DUM, AC, PS, BT, JD, QD, SIZE;
-    __host__ __device__ ContactLayout(int n, int nc, bool tr, int NQ, int NRC)
+    // kmr: register slot capacity of the instantiation (0: slot vectors in LDS, as with torque rows)
+    __host__ __device__ ContactLayout(int n, int nc, bool tr, int NQ, int NRC, int wd, int nfr, double mu, int kmr)
     {
         NJ = tr ? n : 6;
         NR = NJ + 7;
-        ME = NJ + 6 + 3 * nc;
-        NX = n + 3 * nc;
+        WD = wd;
+        NF = wd * nc;
+        NB = NJ + 6 + NF;
+        ME = NB + nfr;
+        MU = mu;
+        NX = n + NF;
         QS = NQ + 1;          // row stride of NQ-wide rows (odd: lane-per-row reads conflict-free)
-        FS = 3 * nc + 1;
+        FS = NF + 1;
         GS = ME | 1;
         TS = (NX + 8) | 1;    // the active set never exceeds NX independent rows (+8: chunked dots)
         int o = 0;
@@ -99,17 +111,17 @@ struct ContactLayout {
             // elimination), so the Gauss-Jordan panel reuses them: 22 KB -> 19.6 KB per instance
             // at n = 30, nc = 2, i.e. 8 instances per CU instead of 7
             const int jcs = 6 * nc * NQ, gjs = 2 * NQ * kGjBS + 2 * kGjBS * NRC;
+            // (with kmr = 0 the T rows of the loop are written only after these are dead)
             ov = jcs > gjs ? jcs : gjs;
             JC = TT;                  // contact Jacobian rows (steps 1-3)
             PN = TT;                  // Gauss-Jordan pivot panel (rows < NQ publish; step 4)
             RH = TT + 2 * NQ * kGjBS;     // its right-hand sides
             HR = TT;                  // (unused: NQ == 64 && tr only)
         }
-        // with torque rows the slot vectors live in LDS: T rows, T columns, Gamma columns
-        // (!tr: scratch for the T_E rows and for dual_gi's re-factorisation, KMR rows of KMR + 1;
-        // KMR = the register slot capacity of launch_nq)
-        const int kmr = nc <= 2 ? 18 : 24;
-        const int tt = tr ? NX * TS : (12 * TS > kmr * (kmr + 1) ? 12 * TS : kmr * (kmr + 1));
+        // with torque rows (or kmr = 0) the slot vectors live in LDS: T rows, T columns, Gamma
+        // columns (else scratch for the T_E rows and for dual_gi's re-factorisation, KMR rows of
+        // KMR + 1; KMR = the register slot capacity of launch_nq)
+        const int tt = (tr || kmr == 0) ? NX * TS : (12 * TS > kmr * (kmr + 1) ? 12 * TS : kmr * (kmr + 1));
         o += tt > ov ? tt : ov;
         XV = o; o += 64;          // x
         X0 = o; o += 64;          // x0 = -H^-1 g
@@ -137,17 +149,36 @@ __device__ __forceinline__ const double *row_q(const double *S, const ContactLay
     return nullptr;
 }
 
-// force coefficient of row ci on force variable f
+// coefficient of friction face k (0..3) on component j (0..2) of its contact's force
+__device__ __forceinline__ double fric_coef(int k, int j, double mu)
+{
+    if (j == 2) return -mu;
+    if (j != (k >> 1)) return 0.0;
+    return (k & 1) ? -1.0 : 1.0;
+}
+
+// force coefficient of row ci on force variable f (FR: the instantiation serves friction rows)
+template <bool FR>
 __device__ __forceinline__ double fcoef(const double *S, const ContactLayout &L, int ci, int f)
 {
     if (ci < L.NJ) return S[L.FFJ + ci * L.FS + f];
     if (ci < L.NJ + 6) return 0.0;
-    return (ci - L.NJ - 6 == f) ? 1.0 : 0.0;
+    if (!FR || ci < L.NB) return (ci - L.NJ - 6 == f) ? 1.0 : 0.0;
+    const int r = ci - L.NB, c = r >> 2, j = f - L.WD * c;
+    return (j >= 0 && j < 3) ? fric_coef(r & 3, j, L.MU) : 0.0;
+}
+
+// activity of friction row ci at the force variables xf (= x + n)
+__device__ __forceinline__ double fric_activity(const double *xf, const ContactLayout &L, int ci)
+{
+    const int r = ci - L.NB, c = r >> 2, k = r & 3;
+    const double *w = xf + L.WD * c;
+    return ((k & 1) ? -1.0 : 1.0) * w[k >> 1] - L.MU * w[2];
 }
 
 // activity a_ci . x of constraint row ci at x = XV (n qdd entries, then nf forces); loads
-// in chunks of 8 so they issue back to back
-template <int NQ>
+// in chunks of 8 so they issue back to back. NFM: the most force variables of the instantiation
+template <int NQ, int NFM, bool FR>
 __device__ __forceinline__ double activity(const double *S, const ContactLayout &L, int ci, int n, int nf)
 {
     const double *xv = S + L.XV;
@@ -168,15 +199,16 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
     const double *fr = S + L.FFJ + (jrow ? ci : 0) * L.FS;
     double sf = 0.0;
 #pragma unroll
-    for (int f = 0; f < 3 * kCMax; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
+    for (int f = 0; f < NFM; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
     if (jrow) return s + sf;
     if (wrow) return s;
+    if (FR && ci >= L.NB) return fric_activity(xv + n, L, ci);
     return xv[n + ci - L.NJ - 6];
 }
 
 // The contact problem for dual_gi: Gamma in LDS, activities from the rows in LDS, and
 // x = x0 + H^-1 A^T w with H^-1 A_q^T from the X^T slots and the diagonal force block.
-template <int NQ, bool TR>
+template <int NQ, bool TR, int NFM, bool FR>
 struct ContactGi {
     // Gamma mixes O(1) acceleration terms with O(1/eps_f) force terms: a force row's genuine
     // complement can sit ~eps_f below its diagonal, so only roundoff-level ones count as
@@ -193,7 +225,7 @@ struct ContactGi {
     __device__ double activity(int r) const
     {
         if constexpr (!TR) {
-            return wbq::activity<NQ>(S, *L, r, n, nf);
+            return wbq::activity<NQ, NFM, FR>(S, *L, r, n, nf);
         } else { // r == this lane's row (dual_gi asks for its own row only)
             const double *xv = S + L->XV;
             const bool jrow = r < L->NJ, wrow = !jrow && r < L->NJ + 6;
@@ -206,9 +238,10 @@ struct ContactGi {
             const double *fr = S + L->FFJ + (jrow ? r : 0) * L->FS;
             double sf = 0.0;
 #pragma unroll
-            for (int f = 0; f < 3 * kCMax; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
+            for (int f = 0; f < NFM; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
             if (jrow) return (s0 + s1) + sf;
             if (wrow) return s0 + s1;
+            if (FR && r >= L->NB) return fric_activity(xv + n, *L, r);
             return xv[n + r - L->NJ - 6];
         }
     }
@@ -228,7 +261,7 @@ struct ContactGi {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int c = cq[u] < L->NJ + 6 ? cq[u] : 0;
-                xq[u] = i < n ? (cq[u] < L->NJ + 6 ? S[L->XT + c * L->QS + i] : 0.0) : fcoef(S, *L, cq[u], fi < 0 ? 0 : fi);
+                xq[u] = i < n ? (cq[u] < L->NJ + 6 ? S[L->XT + c * L->QS + i] : 0.0) : fcoef<FR>(S, *L, cq[u], fi < 0 ? 0 : fi);
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) dx = fma(wq[u], xq[u], dx);
@@ -258,12 +291,15 @@ __device__ __forceinline__ int eq_row(int a, int NJ) { return a < 6 ? a : NJ + a
 // along the unpinned columns, so only a pivot basis of their span (wkeep: a mask of waist rows,
 // from a pivoted Cholesky of their Gram) is kept as level-1 rows -- the others are implied, and
 // keeping them makes the final active set exactly singular.
+// Friction rows (mu > 0) are not boxes in z: the BVLS runs on the box alone and the level-0 point
+// is accepted only if it meets every friction face; otherwise the instance ends with status 2
+// (fricbad: the GPU repair does not solve level 0 over the friction pyramid).
 // Updates this lane's row limits (lo, hi); returns the BVLS iterations, capped = BVLS hit its cap.
 template <int NQ>
 __device__ int contact_level0(const ContactArgs &a, long b, double *S, const ContactLayout &L, int i, double h_i,
-                              double &lo, double &hi, bool &capped, int &wkeep)
+                              double &lo, double &hi, bool &capped, bool &fricbad, int &wkeep)
 {
-    const int n = a.n, nc = a.nc, nf = 3 * nc, na = n - 6;
+    const int n = a.n, nc = a.nc, wd = L.WD, nf = L.NF, na = n - 6;
     const bool qrow = i < n;
     const int ic = qrow ? i : n - 1;
     const long B = a.B;
@@ -300,7 +336,7 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
     {
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
         for (int ff = 0; ff < nf; ++ff) {
-            const int c = ff / 3, k = ff - 3 * c;
+            const int c = ff / wd, k = ff - wd * c;
             const double jv = bload(Jrs, (int)(8 * ic), 8 * (6 * c + k) * n);
 #pragma unroll
             for (int r = 0; r < 6; ++r) {
@@ -314,15 +350,29 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
         zlo = a.torque_rows ? a.tau_min[6 + i] : -kInf;
         zhi = a.torque_rows ? a.tau_max[6 + i] : kInf;
     } else if (fvar) {
-        const int k = f % 3;
-        const bool on = (a.cmask[b] >> (f / 3)) & 1;
-        const double fl = k == 0 ? a.f_lb[0] : (k == 1 ? a.f_lb[1] : a.f_lb[2]);
-        const double fu = k == 0 ? a.f_ub[0] : (k == 1 ? a.f_ub[1] : a.f_ub[2]);
+        const int k = f % wd;
+        const bool on = (a.cmask[b] >> (f / wd)) & 1;
+        double fl = a.w_lb[0], fu = a.w_ub[0];
+#pragma unroll
+        for (int kk = 1; kk < 6; ++kk) {
+            fl = k == kk ? a.w_lb[kk] : fl;
+            fu = k == kk ? a.w_ub[kk] : fu;
+        }
         zlo = on ? fl : 0.0; // an inactive contact's forces are fixed at zero
         zhi = on ? fu : 0.0;
     }
     const bool row = tvar || fvar;
     const BvlsOut bz = bvls<64, 6>(acol, bv, 6, zlo, zhi, row, true, 0, 50 * (na + nf) + 100);
+    fricbad = false;
+    if (a.nfr > 0) { // the friction faces at z* (lane NB + r: face r & 3 of contact r >> 2)
+        const int r = (i >= L.NB && i < L.ME) ? i - L.NB : 0, c = r >> 2, k = r & 3;
+        const double fx = __shfl(bz.xv, na + wd * c), fy = __shfl(bz.xv, na + wd * c + 1);
+        const double fz = __shfl(bz.xv, na + wd * c + 2);
+        const double v = ((k & 1) ? -1.0 : 1.0) * (k < 2 ? fx : fy) - L.MU * fz;
+        const bool on = (a.cmask[b] >> c) & 1;
+        const double tol = 1e-9 * fmax(1.0, fabs(fz));
+        fricbad = imax<64>((i >= L.NB && i < L.ME && on && v > tol) ? 1.0 : 0.0) > 0.0;
+    }
     double ys[6], abm = 0.0, g = 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) ys[r] = isum<64>(row ? acol[r] * bz.xv : 0.0);
@@ -350,7 +400,7 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
     }
     // constraint lanes: torque row a <-> variable a - 6, force row <-> variable na + its force
     const int ci = i;
-    const bool trow = ci >= 6 && ci < L.NJ, frow = ci >= L.NJ + 6 && ci < L.ME;
+    const bool trow = ci >= 6 && ci < L.NJ, frow = ci >= L.NJ + 6 && ci < L.NB;
     const int pin_c = __shfl(pin, trow ? ci - 6 : (frow ? na + ci - L.NJ - 6 : 0));
     if ((trow || frow) && pin_c > 0) lo = hi; // held at the upper limit
     if ((trow || frow) && pin_c < 0) hi = lo; // held at the lower limit
@@ -366,17 +416,23 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
 
 // The whole solve of instance b by one wave (lane i = threadIdx.x). REPAIR (the follow-up
 // kernel): level 0 first (contact_level0: BVLS for y0*, pins), then level 1 with those targets.
-template <int NQ, bool TR, int KMR, bool REPAIR>
+// KMR: register slot capacity (12 + the most force variables; 0 = slot vectors in LDS), WD: wrench
+// components per contact (3 or 6)
+template <int NQ, bool TR, int KMR, int WD, bool REPAIR>
 __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b)
 {
     constexpr int NRC = TR ? 40 : 16; // Gauss-Jordan right-hand sides per pass
-    // the most contacts this instantiation serves (KMR = 18: nc <= 2, launch_nq): the stage then
-    // issues 12 contact-Jacobian loads per lane instead of 24 (a wave's loads stay under the 63
-    // outstanding vector memory operations, as the QPPVM fast kernel's TM)
-    constexpr int CM = (!TR && KMR <= 18) ? 2 : kCMax;
+    // the most contacts this instantiation serves (register slots: KMR = 12 + WD * CM, launch_nq):
+    // with 2 the stage issues 12 contact-Jacobian loads per lane instead of 24 (a wave's loads stay
+    // under the 63 outstanding vector memory operations, as the QPPVM fast kernel's TM)
+    constexpr int CM = (!TR && KMR > 0 && KMR <= 12 + 2 * WD) ? 2 : kCMax;
+    constexpr int NFM = WD * CM; // the most force variables
+    // friction rows only in the LDS-slot instantiations (their ME exceeds the register slots); the
+    // register ones carry none of that code (launch_wd routes mu > 0 to LDS slots)
+    constexpr bool FR = TR || KMR == 0;
     extern __shared__ __attribute__((aligned(16))) double S[];
-    const int n = a.n, nc = a.nc, nf = 3 * nc;
-    const ContactLayout L(n, nc, TR, NQ, NRC);
+    const int n = a.n, nc = a.nc, nf = WD * nc;
+    const ContactLayout L(n, nc, TR, NQ, NRC, WD, FR ? a.nfr : 0, a.mu, TR ? 0 : KMR);
     const int i = threadIdx.x;
     const int cm = a.cmask[b];
     const bool qrow = i < n;
@@ -431,8 +487,8 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
         for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = mrow[r];
 #pragma unroll
-        for (int f = 0; f < 3 * CM; ++f)
-            if (f < nf) S[L.FFJ + i * L.FS + f] = ((cm >> (f / 3)) & 1) ? -jc[6 * (f / 3) + f % 3] : 0.0;
+        for (int f = 0; f < NFM; ++f)
+            if (f < nf) S[L.FFJ + i * L.FS + f] = ((cm >> (f / WD)) & 1) ? -jc[6 * (f / WD) + f % WD] : 0.0;
     }
     if (i < NQ) {
 #pragma unroll
@@ -535,12 +591,22 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     } else if (ci < NJ + 6) {
         kind = 1;
         lo = hi = S[L.BT + ci - NJ];
-    } else if (ci < ME) {
-        const int f = ci - NJ - 6, c = f / 3, k = f - 3 * c;
+    } else if (ci < L.NB) {
+        const int f = ci - NJ - 6, c = f / WD, k = f - WD * c;
         if ((cm >> c) & 1) {
             kind = 2;
-            lo = a.f_lb[k];
-            hi = a.f_ub[k];
+            lo = a.w_lb[0];
+            hi = a.w_ub[0];
+#pragma unroll
+            for (int kk = 1; kk < WD; ++kk) { // (selects: no dynamic index into the kernel arguments)
+                lo = k == kk ? a.w_lb[kk] : lo;
+                hi = k == kk ? a.w_ub[kk] : hi;
+            }
+        }
+    } else if (FR && ci < ME) { // friction face: one-sided
+        if ((cm >> ((ci - L.NB) >> 2)) & 1) {
+            kind = 2;
+            hi = 0.0;
         }
     }
     const double ieps = 1.0 / a.eps_f;
@@ -549,12 +615,12 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
     for (int j = 0; j < NQ; ++j) aq[j] = 0.0;
     if (kind != 0) {
-        double fc[3 * CM];
+        double fc[NFM];
         const double *rq = row_q(S, L, ci);
 #pragma unroll
         for (int j = 0; j < NQ; ++j) aq[j] = rq ? rq[j] : 0.0;
 #pragma unroll
-        for (int f = 0; f < 3 * CM; ++f) fc[f] = f < nf ? fcoef(S, L, ci, f) : 0.0;
+        for (int f = 0; f < NFM; ++f) fc[f] = f < nf ? fcoef<FR>(S, L, ci, f) : 0.0;
         for (int cl = 0; cl < ME; ++cl) {
             double g = 0.0;
             if (cl < NJ + 6) {
@@ -566,12 +632,19 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
             if (cl < NJ) {
                 const double *fr = S + L.FFJ + cl * L.FS;
 #pragma unroll
-                for (int f = 0; f < 3 * CM; ++f)
+                for (int f = 0; f < NFM; ++f)
                     if (f < nf) gf = fma(fc[f], fr[f], gf);
+            } else if (FR && cl >= L.NB) { // friction row cl: its three force coefficients
+                const int r = cl - L.NB, c0 = WD * (r >> 2);
+#pragma unroll
+                for (int f = 0; f < NFM; ++f) {
+                    const int j = f - c0;
+                    if (j >= 0 && j < 3) gf = fma(fc[f], fric_coef(r & 3, j, L.MU), gf);
+                }
             } else if (cl >= NJ + 6) {
                 const int fl = cl - NJ - 6;
 #pragma unroll
-                for (int f = 0; f < 3 * CM; ++f)
+                for (int f = 0; f < NFM; ++f)
                     if (f == fl) gf = fc[f];
             }
             S[L.GM + ci * L.GS + cl] = fma(gf, ieps, g);
@@ -583,13 +656,13 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
     WBQ_STAMP(4);
     int it0 = 0;
-    bool l0cap = false;
+    bool l0cap = false, l0fric = false;
     int wkeep = 0x3f; // waist rows kept as level-1 rows (all, except after a level-0 repair)
     const double lo_free = lo, hi_free = hi, s_x0 = s_i; // (a repair retry restarts from these)
     const int kind_free = kind;
     (void)kind_free;
     if constexpr (REPAIR) { // level 0 not attainable at b_w: y0* and the pins first
-        if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ>(a, b, S, L, i, h_i, lo, hi, l0cap, wkeep);
+        if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ>(a, b, S, L, i, h_i, lo, hi, l0cap, l0fric, wkeep);
         __syncthreads();
     }
 
@@ -598,8 +671,10 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     // lam (its multiplier), aeq (an equality, never dropped), row a and column a of
     // T = L^-1 (Gamma_AA = L L^T, signed normals). Lane j (constraint row j) keeps its
     // activity s_j and GA_j[q] = Gamma[j][act_q].
-    constexpr bool SREG = !TR;      // without torque rows k <= 12 + 3 nc <= KMR: registers
-    constexpr int KM = TR ? 64 : KMR;
+    // without torque rows the active rows are the 12 equalities and independent rows of the
+    // force space: k <= 12 + WD nc <= KMR, in registers (KMR = 0: in LDS, as with torque rows)
+    constexpr bool SREG = !TR && KMR > 0;
+    constexpr int KM = SREG ? KMR : 64;
     using TcolT = typename std::conditional<SREG, SlotVec<KM, true>, TColView>::type;
     using GAT = typename std::conditional<SREG, SlotVec<KM, true>, GAView>::type;
     SlotVec<KM, SREG> Trow;
@@ -644,12 +719,12 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     Tcol.zero_from(0);
     GA.zero_from(0);
     gs = GiState();
-    gs.status = notspd ? 3 : (a.limits_crossed ? 2 : (l0cap ? 1 : 0));
+    gs.status = notspd ? 3 : (a.limits_crossed || l0fric ? 2 : (l0cap ? 1 : 0));
     // rank cap of the loop: the rows never touch the forces of inactive contacts (their rows
     // are disabled, their joint-row coefficients zero), so the rows span at most
-    // n + 3 * (active contacts) dimensions, not nx
-    const int dim = n + 3 * __popc((unsigned)cm & ((1u << nc) - 1u));
-    ContactGi<NQ, TR> pb{S, &L, n, nf, i, ieps, dim};
+    // n + WD * (active contacts) dimensions, not nx
+    const int dim = n + WD * __popc((unsigned)cm & ((1u << nc) - 1u));
+    ContactGi<NQ, TR, NFM, FR> pb{S, &L, n, nf, i, ieps, dim};
     if constexpr (TR) {
 #pragma unroll
         for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
@@ -770,19 +845,19 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         // lane i's own M row and contact-Jacobian column, re-read (L2) rather than held
         const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
         const int moff = (int)(8 * ic);
-        double mr[NQ], jr[3 * CM]; // unconditional (clamped) loads: one round trip
+        double mr[NQ], jr[NFM]; // unconditional (clamped) loads: one round trip
 #pragma unroll
         for (int j = 0; j < NQ; ++j) mr[j] = bload(Mrs, moff, 8 * (j < n ? j : n - 1) * n);
         const __amdgpu_buffer_rsrc_t Jrs = rsrc_at(a.Jc, b, B, (long)nc * 6 * n);
         const int joff = (int)(8 * ic);
 #pragma unroll
-        for (int f = 0; f < 3 * CM; ++f)
-            jr[f] = bload(Jrs, joff, 8 * (6 * (f < nf ? f / 3 : 0) + f % 3) * n);
+        for (int f = 0; f < NFM; ++f)
+            jr[f] = bload(Jrs, joff, 8 * (6 * (f < nf ? f / WD : 0) + f % WD) * n);
 #pragma unroll
         for (int j = 0; j < NQ; ++j) t = fma(j < n ? mr[j] : 0.0, S[L.XV + (j < n ? j : 0)], t);
 #pragma unroll
-        for (int f = 0; f < 3 * CM; ++f)
-            t = fma((f < nf && ((cm >> (f / 3)) & 1)) ? -jr[f] : 0.0, S[L.XV + n + (f < nf ? f : 0)], t);
+        for (int f = 0; f < NFM; ++f)
+            t = fma((f < nf && ((cm >> (f / WD)) & 1)) ? -jr[f] : 0.0, S[L.XV + n + (f < nf ? f : 0)], t);
         tau_i = t;
     }
     const double tmax = imax<64>((qrow && !isfinite(tau_i)) ? 1.0 : 0.0);
@@ -801,15 +876,15 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #endif
 }
 
-template <int NQ, bool TR, int KMR>
-__global__ __launch_bounds__(64, (!TR && KMR <= 18) ? 2 : 1) void contact_kernel(const ContactArgs a)
+template <int NQ, bool TR, int KMR, int WD>
+__global__ __launch_bounds__(64, (!TR && KMR > 0 && KMR <= 18) ? 2 : 1) void contact_kernel(const ContactArgs a)
 {
-    contact_solve<NQ, TR, KMR, false>(a, (long)blockIdx.x);
+    contact_solve<NQ, TR, KMR, WD, false>(a, (long)blockIdx.x);
 }
 
 // Level-0 repair: the instances contact_kernel listed (status -2), grid-stride; its own register
 // budget (the BVLS of the level-0 step) leaves the main kernel's alone.
-template <int NQ, bool TR, int KMR>
+template <int NQ, bool TR, int KMR, int WD>
 __global__ __launch_bounds__(64, 1) void contact_repair_kernel(const ContactArgs a)
 {
     const int cnt = a.work[a.epoch * 2 + 1];
@@ -817,51 +892,60 @@ __global__ __launch_bounds__(64, 1) void contact_repair_kernel(const ContactArgs
         a.work[(a.epoch ^ 1) * 2] = 0;         // by the previous solve, which has completed)
         a.work[(a.epoch ^ 1) * 2 + 1] = 0;
     }
+    follow_publish(a.fg, 0, cnt);
     for (long e = blockIdx.x; e < cnt; e += gridDim.x) {
         __syncthreads(); // the previous instance's LDS is dead
-        contact_solve<NQ, TR, KMR, true>(a, uniform_long(a.wl[e]));
+        contact_solve<NQ, TR, KMR, WD, true>(a, uniform_long(a.wl[e]));
     }
 }
 
-template <int NQ, bool TR, int KMR>
+template <int NQ, bool TR, int KMR, int WD>
 hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {
     constexpr int NRC = TR ? 40 : 16;
-    const ContactLayout L(a.n, a.nc, TR, NQ, NRC);
+    const ContactLayout L(a.n, a.nc, TR, NQ, NRC, WD, a.nfr, a.mu, TR ? 0 : KMR);
     if (L.NR > NRC * ((NQ == 64 && TR) ? 2 : 1) || L.ME > 64 || L.NX > 64) return hipErrorInvalidValue;
-    if (!TR && L.ME > KMR) return hipErrorInvalidValue; // the register slot vectors hold every active row
+    // the register slot vectors hold every active row
+    if (!TR && KMR > 0 && (L.ME > KMR || a.nc * WD > KMR - 12)) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
     if (a.prepare) {
-        const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR>, lds);
-        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR>, lds);
+        const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR, WD>, lds);
+        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR, WD>, lds);
     }
-    hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR, WD>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess || !a.wl) return e2;
     if (mid) {
         e2 = hipEventRecord(mid, stream);
         if (e2 != hipSuccess) return e2;
     }
-    const unsigned grid = a.B < (int)kContactRepairGrid ? (unsigned)a.B : kContactRepairGrid;
-    hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR>), dim3(grid), dim3(64), lds, stream, a);
+    const unsigned grid = follow_blocks(a.fg.est[1], 1, kContactRepairGrid, a.B);
+    hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR, WD>), dim3(grid), dim3(64), lds, stream, a);
     return hipGetLastError();
+}
+
+// Variant by problem shape: torque rows -> LDS slot vectors (k up to n + WD nc); otherwise the
+// active rows fit register slot vectors of 12 + WD nc (18 for the reference's double support,
+// 24 for four contacts or two full wrenches); friction rows (ME > 12 + WD nc) or four full
+// wrenches (36 slots) -> LDS slot vectors.
+template <int NQ, int WD>
+hipError_t launch_wd(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
+{
+    if (a.torque_rows) return launch_t<NQ, true, 64, WD>(a, stream, mid);
+    if (a.nfr > 0) return launch_t<NQ, false, 0, WD>(a, stream, mid);
+    if constexpr (WD == 3)
+        return a.nc <= 2 ? launch_t<NQ, false, 18, 3>(a, stream, mid) : launch_t<NQ, false, 24, 3>(a, stream, mid);
+    else
+        return a.nc <= 2 ? launch_t<NQ, false, 24, 6>(a, stream, mid) : launch_t<NQ, false, 0, 6>(a, stream, mid);
 }
 
 template <int NQ>
 hipError_t launch_nq(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {
-    if (a.torque_rows) return launch_t<NQ, true, 64>(a, stream, mid);
-    return a.nc <= 2 ? launch_t<NQ, false, 18>(a, stream, mid) : launch_t<NQ, false, 24>(a, stream, mid);
+    return a.wd == 6 ? launch_wd<NQ, 6>(a, stream, mid) : launch_wd<NQ, 3>(a, stream, mid);
 }
 
 }  // namespace
-
-size_t contact_lds_bytes(int n, int nc, int torque_rows)
-{
-    const bool tr = torque_rows != 0;
-    const int NQ = n <= 32 ? 32 : 64;
-    return sizeof(double) * ContactLayout(n, nc, tr, NQ, tr ? 40 : 16).SIZE;
-}
 
 hipError_t launch_contact(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
 {

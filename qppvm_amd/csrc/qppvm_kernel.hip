@@ -411,9 +411,13 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 }
 
 // Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by
-// the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set.
+// the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. The work itself
+// is a separate (noinline) function: the kernel's entry is a few instructions that read the count,
+// reset the next solve's counters and exit when there is nothing to do -- a solve with nothing to
+// repair fetches that much code, not the start of the BVLS (the fast kernel's input stream has
+// evicted it from L2 by then).
 template <int NP, int M0>
-__global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
+__device__ __noinline__ void repair_list(const QppvmArgs &a, int cnt)
 {
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -421,11 +425,6 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
-    const int cnt = a.work[a.epoch * 2 + 1]; // instances flagged for the level-0 repair
-    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's counters (its parity was last
-        a.work[(a.epoch ^ 1) * 2] = 0;         // used by the previous solve, which has completed)
-        a.work[(a.epoch ^ 1) * 2 + 1] = 0;
-    }
     for (long e0 = (long)blockIdx.x * IPW; e0 < cnt; e0 += (long)gridDim.x * IPW) {
         const long e = e0 + sub;
         const bool valid = e < cnt;
@@ -434,6 +433,20 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
         __syncthreads(); // the previous instance's LDS is dead
         repair_instance<NP, M0>(a, S, b, i, valid);
     }
+}
+
+template <int NP, int M0>
+__global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
+{
+    constexpr int IPW = kWave / NP;
+    const int cnt = a.work[a.epoch * 2 + 1]; // instances flagged for the level-0 repair
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's counters (its parity was last
+        a.work[(a.epoch ^ 1) * 2] = 0;         // used by the previous solve, which has completed)
+        a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+    }
+    follow_publish(a.fg, a.work[a.epoch * 2], cnt);
+    if ((long)blockIdx.x * IPW >= cnt) return;
+    repair_list<NP, M0>(a, cnt);
 }
 
 // Waves per SIMD of the n > 32 fast kernel (template W). W = 2 caps it at 256 registers (it
@@ -805,14 +818,15 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
         e = hipEventRecord(mid, stream);
         if (e != hipSuccess) return e;
     }
-    // follow-up kernels: grid-stride over their work lists, at most kFollowGrid blocks
-    const unsigned fgrid = grid < kFollowGrid ? grid : kFollowGrid;
+    // follow-up kernels: grid-stride over their work lists, grids sized from the last counts seen
+    const unsigned g1 = follow_blocks(a.fg.est[1], IPW, kFollowGrid, a.B);
     if constexpr (MERGED) {
-        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
     } else {
-        e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, fgrid, stream);
+        const unsigned g0 = follow_blocks(a.fg.est[0], IPW, kFollowGrid, a.B);
+        e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, g0, stream);
         if (e != hipSuccess) return e;
-        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, fgrid, stream);
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
     }
 }
 

@@ -442,6 +442,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
         a.work[(a.epoch ^ 1) * 2] = 0;
         a.work[(a.epoch ^ 1) * 2 + 1] = 0;
     }
+    follow_publish(a.fg, 0, cnt);
     for (int e = blockIdx.x; e < cnt; e += gridDim.x) {
         const long b = a.wl[a.B + e];
         const bool row = i < n;
@@ -505,7 +506,7 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
         e = hipEventRecord(mid, stream);
         if (e != hipSuccess) return e;
     }
-    const unsigned grid = a.B < (int)kFollowGrid ? (unsigned)a.B : kFollowGrid;
+    const unsigned grid = follow_blocks(a.fg.est[1], 1, kFollowGrid, a.B);
     hipLaunchKernelGGL((qppvm_w1m_repair_kernel<NQ, M0, TM>), dim3(grid), dim3(64), lds2, stream, a);
     return hipGetLastError();
 }

@@ -74,6 +74,10 @@ struct wbq_ctx {
     double *jl = nullptr;             // [4][n] joint-limit box: q_min, q_max, Kjl, Djl (JointLimits toggle)
     size_t np = 0;
     int epoch = 0;
+    // follow-up grid sizing (wbq_kernels.h FollowGrid): counts the last follow-up kernel saw, in
+    // mapped pinned host memory (device view work_seen_dev), and the host's running estimate
+    int *work_seen = nullptr, *work_seen_dev = nullptr;
+    int fest[2] = {0, 0};
 };
 
 namespace wbq {
@@ -147,6 +151,29 @@ int hip_fail(wbq_ctx *c, hipError_t e, const char *what)
 int prime_qppvm(wbq_ctx *c);
 int prime_contact(wbq_ctx *c);
 
+// Follow-up grid estimate for the next solve: the counts of the last follow-up launch that has
+// run (relaxed reads of the mapped host block), and at least half the previous estimate.
+wbq::FollowGrid follow_grid(wbq_ctx *c)
+{
+    wbq::FollowGrid fg{};
+    fg.seen = c->work_seen_dev;
+    for (int k = 0; k < 2; ++k) {
+        const int s = c->work_seen ? __atomic_load_n(c->work_seen + k, __ATOMIC_RELAXED) : 0;
+        const int d = c->fest[k] / 2;
+        c->fest[k] = s > d ? s : d;
+        fg.est[k] = c->fest[k];
+    }
+    return fg;
+}
+
+bool alloc_work_seen(wbq_ctx *c)
+{
+    if (hipHostMalloc((void **)&c->work_seen, 2 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return false;
+    c->work_seen[0] = c->work_seen[1] = 0;
+    return hipHostGetDevicePointer((void **)&c->work_seen_dev, c->work_seen, 0) == hipSuccess;
+}
+
 #define WBQ_HIP(call)                                   \
     do {                                                \
         hipError_t e_ = (call);                         \
@@ -170,9 +197,14 @@ int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare)
     a.Kp_p = d.Kp_p;
     a.Kd_p = d.Kd_p;
     a.eps_f = d.eps_f;
+    a.wd = d.wrench_dim == 6 ? 6 : 3;
+    a.mu = d.mu;
+    a.nfr = d.mu > 0.0 ? 4 * d.nc : 0;
     for (int k = 0; k < 3; ++k) {
-        a.f_lb[k] = d.f_lb[k];
-        a.f_ub[k] = d.f_ub[k];
+        a.w_lb[k] = d.f_lb[k];
+        a.w_ub[k] = d.f_ub[k];
+        a.w_lb[3 + k] = d.m_lb[k];
+        a.w_ub[3 + k] = d.m_ub[k];
     }
     a.tau_max = c->tmax;
     a.tau_min = c->tmin;
@@ -202,6 +234,7 @@ int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare)
     a.epoch = c->epoch;
     a.prepare = prepare ? 1 : 0;
     a.ws_rows = c->ws_rows;
+    a.fg = follow_grid(c);
     WBQ_HIP(hipSetDevice(c->device));
     if (prepare) {
         WBQ_HIP(wbq::launch_contact(a, c->stream, nullptr));
@@ -306,7 +339,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess &&
              hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
-             hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
+             alloc_work_seen(c) && hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
              hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
              hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
         if (ok && d.joint_weight == WBQ_WEIGHT_INERTIA) // the dual loop's warm start (dual_gi.h)
@@ -329,17 +362,21 @@ int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
     *out = nullptr;
     const wbq_contact_desc &d = *desc;
     if (d.n_fb != 6 || d.n <= 6 || d.nc < 1 || d.nc > wbq::kCMax || d.max_batch < 1) return WBQ_E_INVALID;
-    if (d.n + 3 * d.nc > 64 || (d.torque_rows ? d.n : 6) + 6 + 3 * d.nc > 64) return WBQ_E_UNSUPPORTED;
+    if (d.wrench_dim != 0 && d.wrench_dim != 3 && d.wrench_dim != 6) return WBQ_E_INVALID;
+    if (!(d.mu >= 0.0)) return WBQ_E_INVALID;
+    const int wd = d.wrench_dim == 6 ? 6 : 3, nfr = d.mu > 0.0 ? 4 * d.nc : 0;
+    // one lane per primal variable and per constraint row
+    if (d.n + wd * d.nc > 64 || (d.torque_rows ? d.n : 6) + 6 + wd * d.nc + nfr > 64) return WBQ_E_UNSUPPORTED;
     if (!(d.eps_f > 0.0)) return WBQ_E_INVALID;
     if (d.torque_rows && (!d.tau_max || !d.tau_min)) return WBQ_E_INVALID;
     for (int k = 0; k < 3; ++k)
-        if (!(d.f_lb[k] <= d.f_ub[k])) return WBQ_E_INVALID;
+        if (!(d.f_lb[k] <= d.f_ub[k]) || (wd == 6 && !(d.m_lb[k] <= d.m_ub[k]))) return WBQ_E_INVALID;
     wbq_ctx *c = new wbq_ctx();
     c->form = WBQ_FORM_CONTACT;
     c->cd = d;
     c->cd.tau_max = c->cd.tau_min = nullptr;
-    c->nx = d.n + 3 * d.nc;
-    const int me = (d.torque_rows ? d.n : 6) + 6 + 3 * d.nc;
+    c->nx = d.n + wd * d.nc;
+    const int me = (d.torque_rows ? d.n : 6) + 6 + wd * d.nc + nfr;
     if (c->cd.max_iter <= 0) c->cd.max_iter = 10 * (c->nx + me) + 50;
     c->d.n = d.n;
     c->d.max_batch = d.max_batch;
@@ -376,7 +413,7 @@ int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out)
               hipHostMalloc((void **)&c->host_out, out_bytes, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->dev_x, B * c->nx * 8) == hipSuccess &&
               hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
-              hipMalloc(&c->wl, B * sizeof(int)) == hipSuccess &&
+              alloc_work_seen(c) && hipMalloc(&c->wl, B * sizeof(int)) == hipSuccess &&
               hipMalloc(&c->ws_rows, B * 64) == hipSuccess && hipMemset(c->ws_rows, 0, B * 64) == hipSuccess &&
               hipEventCreateWithFlags(&c->in_copied, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
@@ -547,6 +584,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.work = c->work;
     a.wl = c->wl;
     a.epoch = c->epoch;
+    a.fg = follow_grid(c);
     a.ws_hint = c->ws_hint;
     a.ws_state = c->ws_state;
     a.ws_rows = c->ws_rows;
@@ -817,6 +855,7 @@ void wbq_destroy(wbq_ctx *c)
     if (c->ui_scr) (void)hipFree(c->ui_scr);
     if (c->b0_scr) (void)hipFree(c->b0_scr);
     if (c->work) (void)hipFree(c->work);
+    if (c->work_seen) (void)hipHostFree(c->work_seen);
     if (c->wl) (void)hipFree(c->wl);
     if (c->ws_hint) (void)hipFree(c->ws_hint);
     if (c->ws_state) (void)hipFree(c->ws_state);

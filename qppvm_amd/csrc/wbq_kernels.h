@@ -8,6 +8,38 @@ constexpr int kWave = 64;
 constexpr int kTMax = 4;    // Cartesian tasks on level 0
 constexpr int kM0Max = 12;  // level-0 rows handled by the kernel
 
+// Follow-up kernels (active set for n > 32, level-0 repair) run grid-stride over device work
+// lists whose length the host never waits for. Their grid is sized from the counts the last
+// follow-up kernel that ran on the context saw (written to mapped host memory, read by the host
+// when it enqueues the next solve; stale by the solves in flight), with headroom and a decay, so
+// a solve with nothing to repair launches a few blocks instead of up to 2,048: the repair kernel's
+// scratch made that empty 2,048-block launch cost 5.2 us of a 38 us config-1 step (rocprofv3,
+// profiles/r02_v15_kernel_stats.csv). The grid size never changes a result: every block loops
+// over the list until it is drained.
+struct FollowGrid {
+    int *seen;    // [2] mapped host memory: counts of the two lists at the last follow-up launch
+    int est[2];   // host estimate of this solve's counts (work items, not blocks)
+};
+constexpr unsigned kFollowMin = 16; // blocks: a count that grows from an estimate of 0 still has 16 waves
+// Blocks for a list of about `est` instances, ipw instances per block, capped by `cap` and the batch.
+inline unsigned follow_blocks(int est, int ipw, unsigned cap, int B)
+{
+    const long want = ((long)est * 5 / 4 + ipw - 1) / ipw + 1;
+    long g = want < (long)kFollowMin ? (long)kFollowMin : want;
+    if (g > (long)cap) g = cap;
+    const long bmax = ((long)B + ipw - 1) / ipw;
+    if (g > bmax) g = bmax;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+// Block 0 of the last follow-up kernel of a solve publishes the counts it saw.
+__device__ __forceinline__ void follow_publish(const FollowGrid &fg, int c0, int c1)
+{
+    if (fg.seen && blockIdx.x == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(fg.seen, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(fg.seen + 1, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Everything one launch needs; passed by value as the kernel argument.
 struct QppvmArgs {
     int B;           // instances
@@ -42,6 +74,7 @@ struct QppvmArgs {
     int *work;       // [2][2] counters: instances appended to the two work lists this solve
     int *wl;         // [2][B] work lists: [0, B) active-set kernel, [B, 2B) repair kernel
     int epoch;       // 0 / 1
+    FollowGrid fg;   // follow-up grid sizing (see FollowGrid)
     // per-instance warm start across solves (the qpOASES hot-start analogue; it changes the
     // path, never the solution): hint = the last solve needed the level-0 repair, so go there
     // directly; state = BVLS bound state (-1/0/+1 per joint) of that repair
@@ -95,8 +128,8 @@ hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t m
 // ------------------------------------------------------------------ contact form (ForceAcc)
 constexpr int kCMax = 4; // contacts
 
-// One launch of the contact-form solve (SURVEY.md 8a rows a10-a12; reference
-// src/ForceAcc.cpp:58-137,181-219). x = [qdd (n); f (3 per contact)].
+// One launch of the contact-form solve (SURVEY.md 8a rows a10-a12, 8f-2; reference
+// src/ForceAcc.cpp:58-137,181-219). x = [qdd (n); w (wd per contact)].
 struct ContactArgs {
     int B;           // instances
     int n;           // DoF incl. the 6 floating-base coordinates (first)
@@ -105,15 +138,18 @@ struct ContactArgs {
     int max_iter;    // active-set step cap
     int limits_crossed;
     double Kp_w, Kd_w, Kp_f, Kd_f, Kp_p, Kd_p; // waist / feet / postural acceleration-task gains
-    double eps_f;                              // min-norm tie-break on the forces
-    double f_lb[3], f_ub[3];                   // force box of an active contact
+    double eps_f;                              // min-norm tie-break on the contact variables
+    int wd;                                    // wrench components per contact: 3 (forces) or 6
+    int nfr;                                   // friction-pyramid rows (4 nc with mu > 0, else 0)
+    double mu;                                 // friction coefficient of the pyramid rows
+    double w_lb[6], w_ub[6];                   // box of an active contact's wd variables
     const double *tau_max, *tau_min;           // [n] (device)
     const double *M, *h, *q, *qd, *qref;       // [B][n][n], [B][n] x4
     const double *Jw, *jdqd_w, *pose_w, *pose_w_ref; // [B][6][n], [B][6], [B][12] x2
     const double *Jc, *jdqd_c, *pose_c, *pose_c_ref; // [B][nc][6][n], [B][nc][6], [B][nc][12] x2
     const int *cmask;                          // [B] bit c = contact c active
     double *tau;     // [B][n]
-    double *x;       // [B][n + 3 nc]
+    double *x;       // [B][n + wd nc]
     int *status;     // [B]
     int *iters;      // [B]
     unsigned long long *stamps; // diagnostic builds (-DWBQ_STAMPS): [B][kStamps] s_memtime
@@ -125,6 +161,7 @@ struct ContactArgs {
     int *work;       // [2][2]
     int *wl;         // [B]
     int epoch;
+    FollowGrid fg;   // repair grid sizing (est[1]; see FollowGrid)
     int prepare;     // as QppvmArgs::prepare
     // warm start: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last
     // solve's final active set, per instance ([B][64]; dual_gi.h warm_start)

@@ -154,6 +154,13 @@ class ContactProblem:
       and (``torque_rows``, row a12, an extension) actuated torque limits;
     * ``tau = M qdd + h - sum_c J_c^T [f_c; 0]`` (``:206-218``).
 
+    SURVEY.md 8f-2 options (defaults = the reference's stack): ``wrench_dim = 6`` makes every
+    contact variable the full wrench ``w_c = [f_c; m_c]`` ("put 6 for full wrench", ``:67``) with
+    the reference's 6-D box ``[f_lb, m_lb] <= w_c <= [f_ub, m_ub]`` (``:74-76``: moments +-1) and
+    ``J_c^T w_c`` over all six Jacobian rows; ``mu > 0`` adds the linearised friction pyramid
+    ``|f_x| <= mu f_z, |f_y| <= mu f_z`` (world frame, four rows per active contact; the reference
+    has no cone).
+
     The acceleration-task gains are OpenSoT defaults upstream (not in the reference); here
     they are named options (critically damped unit stiffness by default).
     """
@@ -170,6 +177,10 @@ class ContactProblem:
     f_lb: tuple = (-1000.0, -1000.0, 10.0)
     f_ub: tuple = (1000.0, 1000.0, 1000.0)
     eps_f: float = 1e-8
+    wrench_dim: int = 3
+    m_lb: tuple = (-1.0, -1.0, -1.0)
+    m_ub: tuple = (1.0, 1.0, 1.0)
+    mu: float = 0.0
     torque_rows: bool = False
     tau_max: np.ndarray | float = 150.0
     tau_min: np.ndarray | float | None = None
@@ -181,19 +192,35 @@ class ContactProblem:
             raise ValueError("nc must be in [1, 4]")
         if self.n_fb != 6 or n <= self.n_fb:
             raise ValueError("the contact form needs a 6-DoF floating base and n > 6")
-        if n + 3 * nc > 64:
-            raise ValueError("n + 3 nc must be <= 64 (one instance per wavefront)")
+        if int(self.wrench_dim) not in (3, 6):
+            raise ValueError("wrench_dim must be 3 or 6")
+        self.wrench_dim = int(self.wrench_dim)
+        if n + self.wrench_dim * nc > 64:
+            raise ValueError("n + wrench_dim * nc must be <= 64 (one instance per wavefront)")
         if not self.eps_f > 0:
             raise ValueError("eps_f must be > 0")
-        self.n, self.nc = n, nc
+        if not self.mu >= 0:
+            raise ValueError("mu must be >= 0")
+        self.n, self.nc, self.mu = n, nc, float(self.mu)
         self.f_lb = tuple(float(v) for v in self.f_lb)
         self.f_ub = tuple(float(v) for v in self.f_ub)
+        self.m_lb = tuple(float(v) for v in self.m_lb)
+        self.m_ub = tuple(float(v) for v in self.m_ub)
         self.tau_max = _vec(self.tau_max, n, "tau_max")
         self.tau_min = -self.tau_max if self.tau_min is None else _vec(self.tau_min, n, "tau_min")
 
     @property
     def nx(self) -> int:
-        return self.n + 3 * self.nc
+        return self.n + self.wrench_dim * self.nc
+
+    @property
+    def w_lb(self) -> tuple:
+        """Box of one active contact's variables (3 forces, or the 6-D wrench)."""
+        return self.f_lb + (self.m_lb if self.wrench_dim == 6 else ())
+
+    @property
+    def w_ub(self) -> tuple:
+        return self.f_ub + (self.m_ub if self.wrench_dim == 6 else ())
 
 
 CONTACT_INPUT_FIELDS = ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref",

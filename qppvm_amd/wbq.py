@@ -55,7 +55,9 @@ class ContactDesc(ctypes.Structure):
                 ("torque_rows", ctypes.c_int), ("max_batch", ctypes.c_int), ("max_iter", ctypes.c_int)] + \
                [(k, ctypes.c_double) for k in ("Kp_w", "Kd_w", "Kp_f", "Kd_f", "Kp_p", "Kd_p")] + \
                [("f_lb", ctypes.c_double * 3), ("f_ub", ctypes.c_double * 3), ("eps_f", ctypes.c_double),
-                ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p)]
+                ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
+                ("wrench_dim", ctypes.c_int), ("m_lb", ctypes.c_double * 3), ("m_ub", ctypes.c_double * 3),
+                ("mu", ctypes.c_double)]
 
 
 _CONTACT_F64 = tuple(k for k in CONTACT_INPUT_FIELDS if k != "cmask")
@@ -311,7 +313,8 @@ class ContactSolver(QPPVMSolver):
     """Batched drop-in for ForceAccExample's per-tick solve (OptvarHelper variables, feet /
     postural / waist acceleration tasks, DynamicFeasibility, wrench bounds, QPOases_sot, and
     the inverse-dynamics post-step; reference src/ForceAcc.cpp:31-141,181-219).
-    Same context semantics as QPPVMSolver; outputs add x = [qdd; f]."""
+    Same context semantics as QPPVMSolver; outputs add x = [qdd; w] (w: 3 forces or the 6-D
+    wrench per contact)."""
 
     def __init__(self, prob: ContactProblem, max_batch: int, device: int = 0):
         self.lib = load_library()
@@ -324,6 +327,8 @@ class ContactSolver(QPPVMSolver):
             setattr(d, k, float(getattr(prob, k)))
         for k in range(3):
             d.f_lb[k], d.f_ub[k] = prob.f_lb[k], prob.f_ub[k]
+            d.m_lb[k], d.m_ub[k] = prob.m_lb[k], prob.m_ub[k]
+        d.wrench_dim, d.mu = prob.wrench_dim, prob.mu
         self._keep = [np.ascontiguousarray(prob.tau_max, dtype=np.float64),
                       np.ascontiguousarray(prob.tau_min, dtype=np.float64)]
         d.tau_max, d.tau_min = _ptr(self._keep[0]), _ptr(self._keep[1])

@@ -46,14 +46,17 @@ def oracle_lib():
     return oracle
 
 
-def load_golden_contact(n):
-    """Yield (group, ContactProblem, inputs, expected) from tests/golden/contact_n{n}.npz."""
+def load_golden_contact(n, fname=None):
+    """Yield (group, ContactProblem, inputs, expected) from tests/golden/contact_n{n}.npz (or
+    fname: contact_ext_n30.npz holds the SURVEY 8f-2 groups, 6-D wrenches and friction rows)."""
     from qppvm_amd.problem import ContactProblem, CONTACT_INPUT_FIELDS
-    z = np.load(os.path.join(GOLDEN, f"contact_n{n}.npz"))
+    z = np.load(os.path.join(GOLDEN, fname or f"contact_n{n}.npz"))
     for g in z["groups"]:
         g = str(g)
         pre = g + "__"
+        ext = {k: (int(z[pre + k]) if k == "wrench_dim" else float(z[pre + k]))
+               for k in ("wrench_dim", "mu") if pre + k in z}
         prob = ContactProblem(n=n, nc=int(z[pre + "nc"]), torque_rows=bool(z[pre + "torque_rows"]),
-                              tau_max=z[pre + "tau_max"])
+                              tau_max=z[pre + "tau_max"], **ext)
         inp = {k: np.ascontiguousarray(z[pre + k]) for k in CONTACT_INPUT_FIELDS}
         yield g, prob, inp, {"tau": z[pre + "tau"], "x": z[pre + "x"]}

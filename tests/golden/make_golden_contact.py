@@ -12,7 +12,8 @@ HIP kernels:
   signs, complementarity) at tight tolerance.
 
 Only instances whose level 0 is attained at the waist target (y0* = b_w) are kept.
-Output: tests/golden/contact_n{30,39}.npz.  Usage: python tests/golden/make_golden_contact.py
+Output: tests/golden/contact_n{30,39}.npz (the reference's point forces) and contact_ext_n30.npz
+(6-D wrenches, friction pyramid).  Usage: python tests/golden/make_golden_contact.py [base] [ext]
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ from qppvm_amd.synth import contact_instances  # noqa: E402
 
 def assemble_np(prob, inp, b):
     n, nc, nfb, nx = prob.n, prob.nc, prob.n_fb, prob.nx
+    wd = prob.wrench_dim
     M, h, q, qd, qref = (inp[k][b] for k in ("M", "h", "q", "qd", "qref"))
 
     def rhs(J, jdqd, pose, pose_ref, Kp, Kd):
@@ -47,29 +49,41 @@ def assemble_np(prob, inp, b):
         bc = rhs(J, inp["jdqd_c"][b, c], inp["pose_c"][b, c], inp["pose_c_ref"][b, c], prob.Kp_f, prob.Kd_f)
         H[:n, :n] += J.T @ J
         g[:n] -= J.T @ bc
-    H[n:, n:] = prob.eps_f * np.eye(3 * nc)
+    H[n:, n:] = prob.eps_f * np.eye(wd * nc)
     bw = rhs(inp["Jw"][b], inp["jdqd_w"][b], inp["pose_w"][b], inp["pose_w_ref"][b], prob.Kp_w, prob.Kd_w)
     E = np.zeros((12, nx))
     E[:6, :n] = inp["Jw"][b]
     E[6:, :n] = M[:nfb]
     for c in range(nc):
-        E[6:, n + 3 * c: n + 3 * c + 3] = -inp["Jc"][b, c, :3, :nfb].T
+        E[6:, n + wd * c: n + wd * c + wd] = -inp["Jc"][b, c, :wd, :nfb].T
     e = np.concatenate([bw, -h[:nfb]])
     rows, lo, hi = [], [], []
     for c in range(nc):
         on = (int(inp["cmask"][b]) >> c) & 1
-        for k in range(3):
+        for k in range(wd):
             r = np.zeros(nx)
-            r[n + 3 * c + k] = 1.0
+            r[n + wd * c + k] = 1.0
             rows.append(r)
-            lo.append(prob.f_lb[k] if on else 0.0)
-            hi.append(prob.f_ub[k] if on else 0.0)
+            lo.append(prob.w_lb[k] if on else 0.0)
+            hi.append(prob.w_ub[k] if on else 0.0)
+    if prob.mu > 0:  # friction pyramid of the active contacts (inactive: forces already zero)
+        for c in range(nc):
+            if not (int(inp["cmask"][b]) >> c) & 1:
+                continue
+            for ax in (0, 1):
+                for sg in (1.0, -1.0):
+                    r = np.zeros(nx)
+                    r[n + wd * c + ax] = sg
+                    r[n + wd * c + 2] = -prob.mu
+                    rows.append(r)
+                    lo.append(-np.inf)
+                    hi.append(0.0)
     if prob.torque_rows:
         for a in range(nfb, n):
             r = np.zeros(nx)
             r[:n] = M[a]
             for c in range(nc):
-                r[n + 3 * c: n + 3 * c + 3] = -inp["Jc"][b, c, :3, a]
+                r[n + wd * c: n + wd * c + wd] = -inp["Jc"][b, c, :wd, a]
             rows.append(r)
             lo.append(prob.tau_min[a] - h[a])
             hi.append(prob.tau_max[a] - h[a])
@@ -85,8 +99,9 @@ def primal_active_set(H, g, E, e, C, lo, hi, maxit=400):
     # strictly interior start (w.r.t. the non-fixed rows): max t s.t. E x = e,
     # lo + t w <= C x <= hi - t w, 0 <= t <= 1; the fixed rows (lo == hi) are equalities
     w = np.where(fixed, 0.0, np.minimum(1.0, (hi - lo) / 4.0))
-    Aub = np.vstack([np.hstack([-C, w[:, None]]), np.hstack([C, w[:, None]])])
-    bub = np.concatenate([-lo, hi])
+    fl = np.isfinite(lo)  # one-sided rows (the friction faces) have no lower side
+    Aub = np.vstack([np.hstack([-C[fl], w[fl, None]]), np.hstack([C, w[:, None]])])
+    bub = np.concatenate([-lo[fl], hi])
     Aeq = np.hstack([E, np.zeros((E.shape[0], 1))])
     cost = np.zeros(nx + 1)
     cost[-1] = -1.0
@@ -169,10 +184,22 @@ GROUPS = [  # name, count, problem kwargs, masks
 ]
 
 
-def make(n, seed):
+# full 6-D wrenches ("put 6 for full wrench", ForceAcc.cpp:67; moment box +-1, :74-76)
+# and the linearised friction pyramid (tests/golden/contact_ext_n30.npz)
+GROUPS_EXT = [
+    ("wrench6_double", 6, dict(nc=2, wrench_dim=6), None),
+    ("wrench6_masks", 6, dict(nc=4, wrench_dim=6), [0b0011, 0b0111, 0b1111, 0b0110, 0b1101]),
+    ("friction_double", 6, dict(nc=2, mu=0.3), None),
+    ("friction_masks", 6, dict(nc=4, mu=0.3), [0b0011, 0b0111, 0b1111, 0b0110, 0b1101]),
+    ("wrench6_friction_torque", 6, dict(nc=2, wrench_dim=6, mu=0.3, torque_rows=True, tau_max=40.0), None),
+    ("friction_torque_masks", 6, dict(nc=4, mu=0.5, torque_rows=True, tau_max=60.0), [0b0011, 0b0111, 0b1111]),
+]
+
+
+def make(n, seed, groups=GROUPS):
     out = {}
     names = []
-    for gi, (name, count, kw, masks) in enumerate(GROUPS):
+    for gi, (name, count, kw, masks) in enumerate(groups):
         prob = ContactProblem(n=n, **kw)
         inp = contact_instances(prob, 4 * count, seed=seed * 100 + gi, masks=masks)
         keep, taus, xs = [], [], []
@@ -188,8 +215,9 @@ def make(n, seed):
             nn, nc = prob.n, prob.nc
             M, h = inp["M"][b], inp["h"][b]
             tau = M @ x[:nn] + h
+            wd = prob.wrench_dim
             for c in range(nc):
-                tau -= inp["Jc"][b, c, :3].T @ x[nn + 3 * c: nn + 3 * c + 3]
+                tau -= inp["Jc"][b, c, :wd].T @ x[nn + wd * c: nn + wd * c + wd]
             nact = int(np.sum(np.minimum(np.abs(a["C"] @ x - a["lo"]), np.abs(a["C"] @ x - a["hi"])) < 1e-8))
             print(f"n={n} {name}[{b}] active_rows={nact} kkt=({stat:.1e},{feas:.1e},{sign:.1e})")
             keep.append(b)
@@ -204,19 +232,26 @@ def make(n, seed):
         out[pre + "x"] = np.array(xs)
         out[pre + "nc"] = np.int32(prob.nc)
         out[pre + "torque_rows"] = np.int32(prob.torque_rows)
+        out[pre + "wrench_dim"] = np.int32(prob.wrench_dim)
+        out[pre + "mu"] = np.float64(prob.mu)
         out[pre + "tau_max"] = prob.tau_max
         names.append(name)
     out["groups"] = np.array(names)
     return out
 
 
-def main():
-    for n, seed in ((30, 4), (39, 5)):
-        data = make(n, seed)
-        path = os.path.join(HERE, f"contact_n{n}.npz")
+def main(which=("base", "ext")):
+    jobs = []
+    if "base" in which:
+        jobs += [(f"contact_n{n}.npz", n, seed, GROUPS) for n, seed in ((30, 4), (39, 5))]
+    if "ext" in which:
+        jobs += [("contact_ext_n30.npz", 30, 6, GROUPS_EXT)]
+    for fname, n, seed, groups in jobs:
+        data = make(n, seed, groups)
+        path = os.path.join(HERE, fname)
         np.savez_compressed(path, **data)
         print("wrote", path, os.path.getsize(path), "bytes")
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or ("base", "ext"))

@@ -18,6 +18,46 @@ def test_contact_oracle_matches_golden(oracle_lib, n):
         assert rel_err(x, exp["x"]) <= 1e-7, (g, rel_err(x, exp["x"]))
 
 
+def test_contact_oracle_matches_golden_ext(oracle_lib):
+    """6-D wrenches (ForceAcc.cpp:67,74-76) and the friction pyramid, against the
+    independent KKT-certified restatement; the friction rows are active in every friction group."""
+    from tests.golden.make_golden_contact import assemble_np
+    for g, prob, inp, exp in load_golden_contact(30, "contact_ext_n30.npz"):
+        tau, x, st, it, rep = oracle_lib.contact_batch(prob, inp)
+        assert np.all(st == 0) and np.all(rep == 0), (g, st, rep)
+        assert rel_err(tau, exp["tau"]) <= 1e-8, (g, rel_err(tau, exp["tau"]))
+        assert rel_err(x, exp["x"]) <= 1e-7, (g, rel_err(x, exp["x"]))
+        if prob.mu > 0:
+            act = 0
+            for b in range(len(st)):
+                a = assemble_np(prob, inp, b)
+                s = a["C"] @ x[b]
+                act += int(np.sum((np.abs(s - a["hi"]) < 1e-8) & ~np.isfinite(a["lo"])))
+            assert act > 0, g
+
+
+def test_contact_wrench6_structure(oracle_lib):
+    """Full wrench: moments within +-1, f_z >= 10, the floating-base torques vanish with
+    tau = M qdd + h - sum J_c^T w_c over all six rows; friction pyramid held."""
+    prob = ContactProblem(n=30, nc=4, wrench_dim=6, mu=0.4)
+    inp = contact_instances(prob, 8, seed=23, masks=[0b0011, 0b0111, 0b1111])
+    tau, x, st, _, _ = oracle_lib.contact_batch(prob, inp)
+    assert np.all(st == 0)
+    n = prob.n
+    for b in range(8):
+        w = x[b, n:].reshape(4, 6)
+        m = int(inp["cmask"][b])
+        t = inp["M"][b] @ x[b, :n] + inp["h"][b] - sum(inp["Jc"][b, c].T @ w[c] for c in range(4))
+        np.testing.assert_allclose(tau[b], t, rtol=0, atol=1e-9 * max(1, np.abs(t).max()))
+        for c in range(4):
+            if (m >> c) & 1:
+                assert w[c, 2] >= 10.0 - 1e-9 and np.abs(w[c, 3:]).max() <= 1.0 + 1e-9
+                assert max(abs(w[c, 0]), abs(w[c, 1])) <= 0.4 * w[c, 2] + 1e-9
+            else:
+                assert np.abs(w[c]).max() <= 1e-12
+        assert np.abs(tau[b, :6]).max() <= 1e-8 * max(1, np.abs(tau[b]).max())
+
+
 def test_contact_structure(oracle_lib):
     """Dynamic feasibility holds, the floating-base torques vanish, inactive feet carry no
     force, active feet push (f_z >= 10), and tau = M qdd + h - sum J_c^T [f; 0]."""
