@@ -215,11 +215,15 @@ const char *wbq_version(void);
  *   getInertiaMatrix      -> M       (used by every task, QPPVMPlugin.cpp:114-118,139,151)
  *   computeNonlinearTerm  -> h       (QPPVMPlugin.cpp:65,312; ForceAcc.cpp:208-217 via ID)
  *   getPose / getJacobian -> pose, J (QPPVMPlugin.cpp:272-284 and the Cartesian tasks :129-152)
- * Model: a kinematic tree of n <= 64 revolute joints, one per link, parent[i] < i (-1 = fixed
- * base); link i's frame is its joint frame, T_i = X_fixed[i] * Rot(axis[i], q_i) in the parent
- * link frame. Outputs use the wbq_inputs layouts (M [B][n][n], h [B][n], J [B][T][6][n] with rows
- * [linear; angular] of the task link's origin in the world frame, pose [B][T][12] = [R | p]), so
- * they feed wbq_set_inputs directly (WBQ_MEM_DEVICE) or wbq_rollout_rbd. */
+ * Model: a kinematic tree of n <= 64 revolute or prismatic joints, one per link, parent[i] < i
+ * (-1 = fixed base); link i's frame is its joint frame, T_i = X_fixed[i] * Rot(axis[i], q_i)
+ * (revolute) or X_fixed[i] * Trans(axis[i] q_i) (prismatic) in the parent link frame. A floating
+ * base is six virtual joints (3 prismatic + 3 revolute, massless links between; the ForceAcc
+ * contact form's n_fb = 6 first coordinates). Task frame t is link task_link[t] times the fixed
+ * task_offset[t] (a frame behind a fixed URDF joint, e.g. a foot sole). Outputs use the wbq_inputs
+ * layouts (M [B][n][n], h [B][n], J [B][T][6][n] with rows [linear; angular] of the task frame's
+ * origin in the world frame, pose [B][T][12] = [R | p], Jdot qd [B][T][6]), so they feed
+ * wbq_set_inputs directly (WBQ_MEM_DEVICE) or wbq_rollout_rbd. */
 typedef struct wbq_rbd_desc {
     int n;
     const int32_t *parent;  /* [n] */
@@ -229,9 +233,12 @@ typedef struct wbq_rbd_desc {
     const double *com;      /* [n][3] link frame */
     const double *inertia;  /* [n][6] Ixx, Iyy, Izz, Ixy, Ixz, Iyz about the COM, link frame */
     double gravity[3];      /* world, e.g. {0, 0, -9.81} */
-    int ntasks;             /* <= 4: the Cartesian task links (their frame origins) */
+    int ntasks;             /* <= 5: the Cartesian task frames (QPPVM: the two arms; contact form:
+                             * the waist, then the contact frames) */
     const int32_t *task_link;
     int max_batch;
+    const int32_t *jtype;       /* [n] 0 revolute, 1 prismatic; NULL = all revolute */
+    const double *task_offset;  /* [ntasks][12] [R | p] in the task link's frame; NULL = identity */
 } wbq_rbd_desc;
 
 typedef struct wbq_rbd_ctx wbq_rbd_ctx;
@@ -242,13 +249,20 @@ int wbq_rbd_create(const wbq_rbd_desc *desc, int device, wbq_rbd_ctx **out);
  * the call waits for the outputs). Any output may be NULL. */
 int wbq_rbd_compute(wbq_rbd_ctx *ctx, int batch, const double *q, const double *qd, double *M, double *h,
                     double *J, double *pose, int memory);
+/* Same plus Jdot qd [B][T][6] of every task frame (the classical acceleration of its origin and the
+ * angular acceleration at qdd = 0, no gravity: XBotInterface computeJdotQdot, ForceAcc.cpp:184 via
+ * the acceleration tasks). */
+int wbq_rbd_compute_ex(wbq_rbd_ctx *ctx, int batch, const double *q, const double *qd, double *M, double *h,
+                       double *J, double *pose, double *jdqd, int memory);
 int wbq_rbd_set_stream(wbq_rbd_ctx *ctx, void *hip_stream);
 void wbq_rbd_destroy(wbq_rbd_ctx *ctx);
 /* MPC rollouts with the model re-evaluated every step: per step, M, h, J and
- * poses of the QPPVM context's inputs are recomputed from its integrated q, qd, then one solve
- * integrates them (wbq_rollout). The QPPVM context must hold device-resident inputs of its own
- * (set with WBQ_MEM_HOST, or WBQ_MEM_DEVICE buffers the caller lets it overwrite) and n, ntasks
- * equal to the model's; both contexts on one device. */
+ * poses of the context's inputs are recomputed from its integrated q, qd, then one solve
+ * integrates them (wbq_rollout). The context must hold device-resident inputs of its own
+ * (set with WBQ_MEM_HOST, or WBQ_MEM_DEVICE buffers the caller lets it overwrite); both contexts on
+ * one device. QPPVM form: the model's n and ntasks equal the context's. Contact form: the model's
+ * tasks are the waist (task 0) and the nc contact frames (tasks 1..nc), which fill Jw, jdqd_w,
+ * pose_w and Jc, jdqd_c, pose_c; n equal (the first 6 joints the floating base). */
 int wbq_rollout_rbd(wbq_ctx *ctx, wbq_rbd_ctx *rbd, int steps, double dt);
 
 #ifdef __cplusplus

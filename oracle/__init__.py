@@ -70,6 +70,8 @@ def lib():
         _lib.wbq_ref_rbd_one.argtypes = [P] * 7
         _lib.wbq_ref_rbd_one.restype = None
         _lib.wbq_ref_rnea.argtypes = [P] * 5
+        _lib.wbq_ref_task_jdqd.argtypes = [P, P, P, I, P]
+        _lib.wbq_ref_task_jdqd.restype = None
         _lib.wbq_ref_rnea.restype = None
     return _lib
 
@@ -268,13 +270,17 @@ class _RbdModel(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("parent", ctypes.c_void_p), ("X_fixed", ctypes.c_void_p),
                 ("axis", ctypes.c_void_p), ("mass", ctypes.c_void_p), ("com", ctypes.c_void_p),
                 ("inertia", ctypes.c_void_p), ("gravity", ctypes.c_double * 3), ("ntasks", ctypes.c_int),
-                ("task_link", ctypes.c_void_p)]
+                ("task_link", ctypes.c_void_p), ("jtype", ctypes.c_void_p), ("task_offset", ctypes.c_void_p)]
 
 
 def _rbd_model(model):
-    """model: qppvm_amd.rbd.RobotModel (or any object with its fields)."""
+    """model: qppvm_amd.rbd.RobotModel (or any object with its fields; jtype / task_offset optional)."""
     keep = {k: np.ascontiguousarray(getattr(model, k), dtype=np.int32 if k in ("parent", "task_link") else np.float64)
             for k in ("parent", "X_fixed", "axis", "mass", "com", "inertia", "task_link")}
+    for k, dt in (("jtype", np.int32), ("task_offset", np.float64)):
+        v = getattr(model, k, None)
+        if v is not None:
+            keep[k] = np.ascontiguousarray(v, dtype=dt)
     m = _RbdModel()
     m.n = int(model.n)
     for k, v in keep.items():
@@ -282,6 +288,20 @@ def _rbd_model(model):
     m.gravity = (ctypes.c_double * 3)(*[float(g) for g in model.gravity])
     m.ntasks = int(len(keep["task_link"]))
     return m, keep
+
+
+def task_jdqd(model, q, qd):
+    """Jdot qd [B][T][6] of every task frame (rows [linear; angular], world frame)."""
+    L = lib()
+    m, keep = _rbd_model(model)
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+    qd = np.ascontiguousarray(np.atleast_2d(qd), dtype=np.float64)
+    B, T = q.shape[0], len(model.task_link)
+    out = np.zeros((B, T, 6))
+    for b in range(B):
+        for t in range(T):
+            L.wbq_ref_task_jdqd(ctypes.byref(m), _p(q[b]), _p(qd[b]), t, _p(out[b, t]))
+    return out
 
 
 def rbd_batch(model, q, qd):

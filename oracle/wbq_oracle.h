@@ -174,10 +174,12 @@ void wbq_ref_contact_batch(const wbq_ref_contact_desc *d, int B, const double *M
                            const double *pose_c, const double *pose_c_ref, const int32_t *cmask, double *tau,
                            double *x, int32_t *status, int32_t *iters, int32_t *l0_repaired);
 
-/* ---- rigid-body dynamics (oracle/wbq_oracle_rbd.c): kinematic tree of revolute joints, one
- * per link, parent[i] < i (-1 = fixed base); link frame = joint frame,
- * T_i = X_fixed[i] Rot(axis[i], q_i) in the parent link frame. Same fields as wbq_rbd_desc
- * (include/wbq.h). */
+/* ---- rigid-body dynamics (oracle/wbq_oracle_rbd.c): kinematic tree of revolute or prismatic
+ * joints, one per link, parent[i] < i (-1 = fixed base); link frame = joint frame,
+ * T_i = X_fixed[i] Rot(axis[i], q_i) (revolute) or X_fixed[i] Trans(axis[i] q_i) (prismatic) in the
+ * parent link frame; a floating base is six such joints (3 prismatic + 3 revolute, massless
+ * intermediate links). Task frame t = link task_link[t] times task_offset[t]. Same fields as
+ * wbq_rbd_desc (include/wbq.h). */
 #define WBQ_REF_RBD_MAX 64
 typedef struct {
     int n;
@@ -190,11 +192,16 @@ typedef struct {
     double gravity[3];
     int ntasks;
     const int *task_link;   /* [ntasks] */
+    const int *jtype;       /* [n] 0 revolute, 1 prismatic; NULL = all revolute */
+    const double *task_offset; /* [ntasks][12] [R | p] in the task link's frame; NULL = identity */
 } wbq_ref_rbd_model;
 
 void wbq_ref_rnea(const wbq_ref_rbd_model *m, const double *q, const double *qd, const double *qdd, double *tau);
 void wbq_ref_crba(const wbq_ref_rbd_model *m, const double *q, double *M);
 void wbq_ref_link_kinematics(const wbq_ref_rbd_model *m, const double *q, int e, double *pose, double *J);
+/* Jdot qd of task frame t (the classical acceleration of its origin and the angular acceleration
+ * at qdd = 0, no gravity; rows [linear; angular], world frame): XBotInterface computeJdotQdot. */
+void wbq_ref_task_jdqd(const wbq_ref_rbd_model *m, const double *q, const double *qd, int t, double *jdqd);
 void wbq_ref_rbd_one(const wbq_ref_rbd_model *m, const double *q, const double *qd, double *M, double *h,
                      double *J, double *pose);
 

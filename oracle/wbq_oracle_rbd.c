@@ -10,9 +10,11 @@
  * Dynamics Algorithms", 2008: RNEA Table 5.1, CRBA Table 6.2); the GPU kernel uses world-frame
  * sums over ancestor sets instead, so the two share no algorithm.
  *
- * Model: a kinematic tree of n revolute joints, one per link, parent[i] < i (-1 = fixed base).
- * Link i's frame is the joint frame: T_i = X_fixed[i] * Rot(axis[i], q_i) relative to the parent
- * link frame. Spatial vectors [angular; linear]. */
+ * Model: a kinematic tree of n revolute or prismatic joints, one per link, parent[i] < i (-1 =
+ * fixed base). Link i's frame is the joint frame: T_i = X_fixed[i] * Rot(axis[i], q_i) (revolute)
+ * or X_fixed[i] * Trans(axis[i] q_i) (prismatic) relative to the parent link frame; motion subspace
+ * S_i = [axis; 0] or [0; axis]. Task frame t = link task_link[t] * task_offset[t]. Spatial vectors
+ * [angular; linear]. */
 #include <math.h>
 #include <string.h>
 
@@ -127,6 +129,26 @@ static void mat6_vec(const double *A, const double *v, double *out)
     }
 }
 
+static int prismatic(const wbq_ref_rbd_model *m, int i) { return m->jtype && m->jtype[i] == 1; }
+
+/* motion subspace of joint i in its link frame */
+static void subspace(const wbq_ref_rbd_model *m, int i, double *S)
+{
+    const double *a = m->axis + 3 * i;
+    const int pr = prismatic(m, i);
+    for (int r = 0; r < 3; ++r) {
+        S[r] = pr ? 0.0 : a[r];
+        S[3 + r] = pr ? a[r] : 0.0;
+    }
+}
+
+static double dot6(const double *a, const double *b)
+{
+    double s = 0.0;
+    for (int k = 0; k < 6; ++k) s += a[k] * b[k];
+    return s;
+}
+
 static void local_transforms(const wbq_ref_rbd_model *m, const double *q, se3 *T)
 {
     for (int i = 0; i < m->n; ++i) {
@@ -135,8 +157,13 @@ static void local_transforms(const wbq_ref_rbd_model *m, const double *q, se3 *T
             for (int c = 0; c < 3; ++c) F.R[3 * r + c] = m->X_fixed[12 * i + 4 * r + c];
             F.p[r] = m->X_fixed[12 * i + 4 * r + 3];
         }
-        rot_axis(m->axis + 3 * i, q[i], Jq.R);
-        Jq.p[0] = Jq.p[1] = Jq.p[2] = 0.0;
+        if (prismatic(m, i)) {
+            for (int k = 0; k < 9; ++k) Jq.R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+            for (int r = 0; r < 3; ++r) Jq.p[r] = m->axis[3 * i + r] * q[i];
+        } else {
+            rot_axis(m->axis + 3 * i, q[i], Jq.R);
+            Jq.p[0] = Jq.p[1] = Jq.p[2] = 0.0;
+        }
         T[i] = compose(&F, &Jq);
     }
 }
@@ -152,7 +179,8 @@ void wbq_ref_rnea(const wbq_ref_rbd_model *m, const double *q, const double *qd,
     const double v0[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
         const int p = m->parent[i];
-        double S[6] = {m->axis[3 * i], m->axis[3 * i + 1], m->axis[3 * i + 2], 0, 0, 0}, t[6], c[6], I[36], Iv[6];
+        double S[6], t[6], c[6], I[36], Iv[6];
+        subspace(m, i, S);
         xform_motion(&T[i], p < 0 ? v0 : v[p], v[i]);
         for (int k = 0; k < 6; ++k) v[i][k] += S[k] * qd[i];
         xform_motion(&T[i], p < 0 ? a0 : a[p], a[i]);
@@ -166,8 +194,9 @@ void wbq_ref_rnea(const wbq_ref_rbd_model *m, const double *q, const double *qd,
         for (int k = 0; k < 6; ++k) f[i][k] += t[k];
     }
     for (int i = n - 1; i >= 0; --i) {
-        const double *ax = m->axis + 3 * i;
-        tau[i] = ax[0] * f[i][0] + ax[1] * f[i][1] + ax[2] * f[i][2];
+        double S[6];
+        subspace(m, i, S);
+        tau[i] = dot6(S, f[i]);
         const int p = m->parent[i];
         if (p >= 0) {
             double fp[6];
@@ -211,47 +240,108 @@ void wbq_ref_crba(const wbq_ref_rbd_model *m, const double *q, double *M)
         }
     }
     for (int i = 0; i < n; ++i) {
-        const double S[6] = {m->axis[3 * i], m->axis[3 * i + 1], m->axis[3 * i + 2], 0, 0, 0};
-        double F[6];
+        double S[6], F[6];
+        subspace(m, i, S);
         mat6_vec(Ic[i], S, F);
-        M[i * n + i] = S[0] * F[0] + S[1] * F[1] + S[2] * F[2];
+        M[i * n + i] = dot6(S, F);
         int j = i;
         while (m->parent[j] >= 0) {
             double Fp[6];
             xform_force_T(&T[j], F, Fp);
             memcpy(F, Fp, sizeof F);
             j = m->parent[j];
-            const double *aj = m->axis + 3 * j;
-            const double v = aj[0] * F[0] + aj[1] * F[1] + aj[2] * F[2];
+            double Sj[6];
+            subspace(m, j, Sj);
+            const double v = dot6(Sj, F);
             M[i * n + j] = v;
             M[j * n + i] = v;
         }
     }
 }
 
-/* World poses of every link; task pose [R | p] row-major 3 x 4 and the geometric Jacobian
- * (rows: linear velocity of the link origin, angular velocity; world frame) of link e. */
-void wbq_ref_link_kinematics(const wbq_ref_rbd_model *m, const double *q, int e, double *pose, double *J)
+static se3 task_offset(const wbq_ref_rbd_model *m, int t)
+{
+    se3 X;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) X.R[3 * r + c] = m->task_offset ? m->task_offset[12 * t + 4 * r + c] : (r == c);
+        X.p[r] = m->task_offset ? m->task_offset[12 * t + 4 * r + 3] : 0.0;
+    }
+    return X;
+}
+
+/* World pose [R | p] row-major 3 x 4 and the geometric Jacobian (rows: linear velocity of the
+ * frame origin, angular velocity; world frame) of the frame Xo attached to link e. */
+static void frame_kinematics(const wbq_ref_rbd_model *m, const double *q, int e, const se3 *Xo, double *pose, double *J)
 {
     const int n = m->n;
     se3 T[WBQ_REF_RBD_MAX], W[WBQ_REF_RBD_MAX];
     local_transforms(m, q, T);
     for (int i = 0; i < n; ++i) W[i] = m->parent[i] < 0 ? T[i] : compose(&W[m->parent[i]], &T[i]);
+    const se3 We = compose(&W[e], Xo);
     for (int r = 0; r < 3; ++r) {
-        for (int c = 0; c < 3; ++c) pose[4 * r + c] = W[e].R[3 * r + c];
-        pose[4 * r + 3] = W[e].p[r];
+        for (int c = 0; c < 3; ++c) pose[4 * r + c] = We.R[3 * r + c];
+        pose[4 * r + 3] = We.p[r];
     }
     memset(J, 0, sizeof(double) * 6 * n);
     for (int j = e; j >= 0; j = m->parent[j]) {
         double a[3], d[3], lin[3];
         for (int r = 0; r < 3; ++r)
             a[r] = W[j].R[3 * r] * m->axis[3 * j] + W[j].R[3 * r + 1] * m->axis[3 * j + 1] + W[j].R[3 * r + 2] * m->axis[3 * j + 2];
-        for (int r = 0; r < 3; ++r) d[r] = W[e].p[r] - W[j].p[r];
+        if (prismatic(m, j)) {
+            for (int r = 0; r < 3; ++r) {
+                J[r * n + j] = a[r];
+                J[(3 + r) * n + j] = 0.0;
+            }
+            continue;
+        }
+        for (int r = 0; r < 3; ++r) d[r] = We.p[r] - W[j].p[r];
         cross3(a, d, lin);
         for (int r = 0; r < 3; ++r) {
             J[r * n + j] = lin[r];
             J[(3 + r) * n + j] = a[r];
         }
+    }
+}
+
+void wbq_ref_link_kinematics(const wbq_ref_rbd_model *m, const double *q, int e, double *pose, double *J)
+{
+    const se3 I = {{1, 0, 0, 0, 1, 0, 0, 0, 1}, {0, 0, 0}};
+    frame_kinematics(m, q, e, &I, pose, J);
+}
+
+/* Jdot qd of task frame t: the link-coordinate forward pass with qdd = 0 and no gravity gives the
+ * task link's spatial velocity v = [w; v_O] and acceleration a = [dw; a_O] at its origin; the frame
+ * origin p (link coordinates) then has classical acceleration a_O + dw x p + w x (v_O + w x p). */
+void wbq_ref_task_jdqd(const wbq_ref_rbd_model *m, const double *q, const double *qd, int t, double *jdqd)
+{
+    const int n = m->n, e = m->task_link[t];
+    se3 T[WBQ_REF_RBD_MAX], W[WBQ_REF_RBD_MAX];
+    double v[WBQ_REF_RBD_MAX][6], a[WBQ_REF_RBD_MAX][6];
+    local_transforms(m, q, T);
+    for (int i = 0; i < n; ++i) W[i] = m->parent[i] < 0 ? T[i] : compose(&W[m->parent[i]], &T[i]);
+    const double z6[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i <= e; ++i) {
+        const int p = m->parent[i];
+        double S[6], sq[6], c[6];
+        subspace(m, i, S);
+        xform_motion(&T[i], p < 0 ? z6 : v[p], v[i]);
+        for (int k = 0; k < 6; ++k) v[i][k] += S[k] * qd[i];
+        xform_motion(&T[i], p < 0 ? z6 : a[p], a[i]);
+        for (int k = 0; k < 6; ++k) sq[k] = S[k] * qd[i];
+        crm(v[i], sq, c);
+        for (int k = 0; k < 6; ++k) a[i][k] += c[k];
+    }
+    const se3 Xo = task_offset(m, t);
+    const double *w = v[e], *vo = v[e] + 3, *dw = a[e], *ao = a[e] + 3, *p = Xo.p;
+    double t1[3], t2[3], vp[3], t3[3], lin[3];
+    cross3(dw, p, t1);
+    cross3(w, p, t2);
+    for (int r = 0; r < 3; ++r) vp[r] = vo[r] + t2[r];
+    cross3(w, vp, t3);
+    for (int r = 0; r < 3; ++r) lin[r] = ao[r] + t1[r] + t3[r];
+    for (int r = 0; r < 3; ++r) {
+        jdqd[r] = W[e].R[3 * r] * lin[0] + W[e].R[3 * r + 1] * lin[1] + W[e].R[3 * r + 2] * lin[2];
+        jdqd[3 + r] = W[e].R[3 * r] * dw[0] + W[e].R[3 * r + 1] * dw[1] + W[e].R[3 * r + 2] * dw[2];
     }
 }
 
@@ -263,6 +353,8 @@ void wbq_ref_rbd_one(const wbq_ref_rbd_model *m, const double *q, const double *
     memset(zero, 0, sizeof zero);
     wbq_ref_crba(m, q, M);
     wbq_ref_rnea(m, q, qd, zero, h);
-    for (int t = 0; t < m->ntasks; ++t)
-        wbq_ref_link_kinematics(m, q, m->task_link[t], pose + 12 * t, J + (size_t)6 * m->n * t);
+    for (int t = 0; t < m->ntasks; ++t) {
+        const se3 Xo = task_offset(m, t);
+        frame_kinematics(m, q, m->task_link[t], &Xo, pose + 12 * t, J + (size_t)6 * m->n * t);
+    }
 }

@@ -441,7 +441,8 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
         if (need_select) {
             double v = -1.0;
             if (kind == 2 && !g.onact) {
-                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fabs(lo), fabs(hi))));
+                // (an unbounded side, +-kInf -- the one-sided friction faces -- does not scale it)
+                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s_i), fmax(fin_abs(lo), fin_abs(hi))));
                 const double viol = fmax(lo - s_i, s_i - hi);
                 if (viol > tol) v = viol / nrm;
             }

@@ -412,10 +412,11 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 
 // Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by
 // the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. The work itself
-// is a separate (noinline) function: the kernel's entry is a few instructions that read the count,
-// reset the next solve's counters and exit when there is nothing to do -- a solve with nothing to
-// repair fetches that much code, not the start of the BVLS (the fast kernel's input stream has
-// evicted it from L2 by then).
+// is a separate (noinline) function, so the kernel's entry is only the count read, the counter
+// reset and the exit. Measured (r03, rocprofv3): an empty launch still takes ~5 us after the fast
+// kernel, with 16 blocks as with 2,048 and with or without this split, while no-work kernels with
+// the same registers / LDS / scratch / stores add ~1.7 us (scripts/launch_probe2.hip): the cost is
+// the dependent kernarg -> counter load chain after the fast kernel's input stream evicted L2.
 template <int NP, int M0>
 __device__ __noinline__ void repair_list(const QppvmArgs &a, int cnt)
 {

@@ -180,7 +180,7 @@ bool alloc_work_seen(wbq_ctx *c)
         if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
     } while (0)
 
-int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare)
+int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare, const wbq_rbd_ctx *rbd = nullptr)
 {
     const wbq_contact_desc &d = c->cd;
     wbq::ContactArgs a{};
@@ -243,6 +243,12 @@ int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare)
     const bool timed = c->timing && a.B > 0 && c->ev_used + 3 <= (int)c->ev.size() &&
                        (c->solves++ % (unsigned long long)c->timing_every) == 0;
     if (timed) WBQ_HIP(hipEventRecord(c->ev[c->ev_used], c->stream));
+    if (rbd) // the model at the integrated state: M, h, the waist (task 0) and contact frames (tasks 1..nc)
+        WBQ_HIP(wbq::rbd_launch_split(rbd, c->batch, c->in[2], c->in[3], const_cast<double *>(c->in[0]),
+                                      const_cast<double *>(c->in[1]), 1, const_cast<double *>(c->in[5]),
+                                      const_cast<double *>(c->in[7]), const_cast<double *>(c->in[6]),
+                                      const_cast<double *>(c->in[9]), const_cast<double *>(c->in[11]),
+                                      const_cast<double *>(c->in[10]), c->stream));
     WBQ_HIP(wbq::launch_contact(a, c->stream, timed ? c->ev[c->ev_used + 1] : nullptr));
     if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
     if (timed) {
@@ -547,7 +553,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
         WBQ_HIP(hipStreamWaitEvent(c->stream, c->in_copied, 0));
         c->in_stream = c->stream;
     }
-    if (c->form == WBQ_FORM_CONTACT) return solve_contact(c, integrate, dt, prepare);
+    if (c->form == WBQ_FORM_CONTACT) return solve_contact(c, integrate, dt, prepare, rbd);
     wbq::QppvmArgs a{};
     a.B = c->batch;
     a.n = c->d.n;
@@ -638,10 +644,11 @@ int wbq_rollout(wbq_ctx *c, int steps, double dt)
 int wbq_rollout_rbd(wbq_ctx *c, wbq_rbd_ctx *rbd, int steps, double dt)
 {
     if (!c || !rbd) return WBQ_E_INVALID;
-    if (c->form != WBQ_FORM_QPPVM) return fail(c, WBQ_E_UNSUPPORTED, "wbq_rollout_rbd: QPPVM form only");
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
-    if (wbq::rbd_n(rbd) != c->d.n || wbq::rbd_ntasks(rbd) != c->d.ntasks || wbq::rbd_device(rbd) != c->device)
-        return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: model n / ntasks / device differ from the context's");
+    const int want_t = c->form == WBQ_FORM_CONTACT ? 1 + c->cd.nc : c->d.ntasks;
+    if (wbq::rbd_n(rbd) != c->d.n || wbq::rbd_ntasks(rbd) != want_t || wbq::rbd_device(rbd) != c->device)
+        return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: model n / tasks / device differ from the context's "
+                                      "(contact form: the waist and the nc contact frames)");
     if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: steps >= 0, dt >= 0");
     WBQ_HIP(hipSetDevice(c->device));
     if (c->in_pending && c->in_stream != c->stream) {

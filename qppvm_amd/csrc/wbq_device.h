@@ -8,6 +8,9 @@ namespace wbq {
 
 constexpr double kInf = 1.0e300;
 
+// |v| of a finite bound, 0 for an unbounded side (+-kInf): tolerances scale with finite bounds only
+__device__ __forceinline__ double fin_abs(double v) { return fabs(v) < 1.0e299 ? fabs(v) : 0.0; }
+
 // Phase stamps for the diagnostic build only (never compiled into the product library).
 #ifdef WBQ_STAMPS
 #define WBQ_STAMP(k)                                                                    \

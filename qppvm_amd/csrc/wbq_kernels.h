@@ -194,6 +194,11 @@ namespace wbq {
 // layouts (any may be null).
 hipError_t rbd_launch(const wbq_rbd_ctx *c, int B, const double *q, const double *qd, double *M, double *h, double *J,
                       double *pose, hipStream_t stream);
+// tasks [0, split) into (J, pose, jdqd), tasks [split, ntasks) into (J2, pose2, jdqd2) (the contact
+// form's waist and contact arrays)
+hipError_t rbd_launch_split(const wbq_rbd_ctx *c, int B, const double *q, const double *qd, double *M, double *h,
+                            int split, double *J, double *pose, double *jdqd, double *J2, double *pose2, double *jdqd2,
+                            hipStream_t stream);
 int rbd_n(const wbq_rbd_ctx *c);
 int rbd_ntasks(const wbq_rbd_ctx *c);
 int rbd_device(const wbq_rbd_ctx *c);

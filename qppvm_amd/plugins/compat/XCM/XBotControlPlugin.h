@@ -3,7 +3,8 @@
 // only the API the reference plugins call, with the reference's own
 // spellings, so the shells contain nothing a real XCM + XBotInterface + Eigen + KDL build would
 // reject:
-//   Eigen   VectorXd (Zero, Constant, setZero, setConstant, arithmetic), MatrixXd, Matrix3d,
+//   Eigen   VectorXd (Zero, Constant, setZero, setConstant, arithmetic, the << comma initializer),
+//           MatrixXd, Matrix3d,
 //           Matrix4d, Vector3d (Zero, UnitZ), Vector6d (XBotInterface's typedef),
 //           Affine3d (linear(), translation(), matrix())
 //   KDL     Frame {M, p}, Vector (x()/y()/z() getters and setters: QPPVMPlugin.cpp:219-221)
@@ -34,6 +35,18 @@
 namespace Eigen {
 
 using Index = std::ptrdiff_t;
+
+// comma initializer (v << a, b, c, ...): coefficients in row-major order, as Eigen fills them
+template <class D>
+struct CommaInitializer {
+    D &m;
+    Index k;
+    CommaInitializer &operator,(double v)
+    {
+        m.comma_set(k++, v);
+        return *this;
+    }
+};
 
 // fixed-size dense matrix, column-major like Eigen::Matrix<double, R, C>
 template <int R, int C>
@@ -89,6 +102,12 @@ public:
     friend Matrix operator*(double s, const Matrix &m) { return m * s; }
     Matrix &operator+=(const Matrix &o) { return *this = *this + o; }
     Matrix &operator-=(const Matrix &o) { return *this = *this - o; }
+    CommaInitializer<Matrix> operator<<(double v)
+    {
+        comma_set(0, v);
+        return CommaInitializer<Matrix>{*this, 1};
+    }
+    void comma_set(Index k, double v) { (*this)(k / C, k % C) = v; }
 
 private:
     Matrix zip(const Matrix &o, double s) const
@@ -137,6 +156,12 @@ public:
     double operator()(Index i) const { return d_[(std::size_t)i]; }
     double *data() { return d_.data(); }
     const double *data() const { return d_.data(); }
+    CommaInitializer<VectorXd> operator<<(double v)
+    {
+        comma_set(0, v);
+        return CommaInitializer<VectorXd>{*this, 1};
+    }
+    void comma_set(Index k, double v) { d_.at((std::size_t)k) = v; }
     VectorXd operator+(const VectorXd &o) const { return zip(o, 1.0); }
     VectorXd operator-(const VectorXd &o) const { return zip(o, -1.0); }
     VectorXd operator-() const { return *this * -1.0; }

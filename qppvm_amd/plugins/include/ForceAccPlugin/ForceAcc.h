@@ -40,6 +40,12 @@ public:
     int contact_mask() const { return _cmask; }
     // the reference hard-codes "/tmp/opensot_force_acc_example" (ForceAcc.cpp:34)
     void set_log_prefix(const std::string &prefix) { _log_prefix = prefix; }
+    // SURVEY 8f-2 options, set before init_control_plugin: 6 = the full-wrench variables the
+    // reference comments on ("put 6 for full wrench", ForceAcc.cpp:67; its 6-D box :74-76);
+    // mu > 0 = the linearised friction pyramid (no cone in the reference)
+    void set_wrench_dim(int wd) { _wd = wd == 6 ? 6 : 3; }
+    void set_friction(double mu) { _mu = mu; }
+    int wrench_dim() const { return _wd; }
 
 protected:
     void control_loop(double time, double period) override;
@@ -56,11 +62,13 @@ private:
     int _iters = 0;
     int _solver_errors = 0;
     int _cmask = 0xF;
+    int _wd = 3;       // variables per contact: 3 forces (:67) or the 6-D wrench
+    double _mu = 0.0;  // friction pyramid coefficient (0: none, the reference)
 
     Eigen::VectorXd _k, _d, _q, _qdot, _q_ref, _tau, _tau_c, _x, _qddot_value, _h;
     Eigen::Vector3d _initial_com; // ForceAcc.h:69 (the pelvis origin, ForceAcc.cpp:164)
     Eigen::MatrixXd _Mtmp, _Jtmp;
-    std::vector<Eigen::VectorXd> _wrench_value; // [f_c; 0] per contact (ForceAcc.cpp:61,199)
+    std::vector<Eigen::VectorXd> _wrench_value; // [f_c; 0] (or the 6-D wrench) per contact (ForceAcc.cpp:61,199)
     Eigen::Affine3d _waist_ref;
     std::vector<Eigen::Affine3d> _feet_ref;
     std::vector<std::string> _contact_links{"foot_fl", "foot_fr", "foot_hr", "foot_hl"}; // ForceAcc.cpp:58

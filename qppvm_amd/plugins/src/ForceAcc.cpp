@@ -40,6 +40,7 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
     _model->initLog(_logger, 10000); // :50
 
     // stack wiring (:58-137): x = [qddot; f_c x 4], wrench bounds (-1000,-1000,10)..(1000,..),
+    // (with set_wrench_dim(6): x = [qddot; w_c x 4] boxed by the full 6-D bounds)
     // waist / (postural + feet) << dyn_feas << wrench bounds; the acceleration-task gains are
     // OpenSoT defaults upstream, here the build's named defaults (critically damped, Kp = 1)
     const int n = _model->getJointNum();
@@ -52,11 +53,17 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
     d.max_batch = 1;
     d.Kp_w = d.Kp_f = d.Kp_p = 1.0;
     d.Kd_w = d.Kd_f = d.Kd_p = 2.0;
-    const double lb[3] = {-1000.0, -1000.0, 10.0}, ub[3] = {1000.0, 1000.0, 1000.0}; // :74-76
+    Eigen::VectorXd wrench_ub(6), wrench_lb(6); // :74-76
+    wrench_ub << 1000, 1000, 1000, 1, 1, 1;
+    wrench_lb << -1000, -1000, 10, -1, -1, -1;
     for (int k = 0; k < 3; ++k) {
-        d.f_lb[k] = lb[k];
-        d.f_ub[k] = ub[k];
+        d.f_lb[k] = wrench_lb[k];
+        d.f_ub[k] = wrench_ub[k];
+        d.m_lb[k] = wrench_lb[3 + k]; // bound only with the full wrench (wrench_dim 6)
+        d.m_ub[k] = wrench_ub[3 + k];
     }
+    d.wrench_dim = _wd; // :67 vars.emplace_back(cl, 3) -- "put 6 for full wrench"
+    d.mu = _mu;
     d.eps_f = 1e-8; // explicit min-norm tie-break of the internal forces
     const int rc = wbq_create_contact(&d, 0, &_ctx);
     if (rc != WBQ_SUCCESS) {
@@ -68,7 +75,7 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
                               nc * 6 * n, nc * 6, nc * 12, nc * 12};
     for (int f = 0; f < 13; ++f) _in[f].assign(sizes[f], 0.0);
     _feet_ref.resize(nc);
-    _x.setZero(n + 3 * nc);
+    _x.setZero(n + _wd * (int)nc);
     _tau.setZero(n);
     _tau_c.setZero(n);
     _qddot_value.setZero(n);
@@ -77,7 +84,7 @@ bool ForceAccExample::init_control_plugin(XBot::Handle::Ptr handle) // :31-141
     _logger->createVectorVariable("tau", n, 1, 10000);
     _logger->createVectorVariable("tau_c", n, 1, 10000);
     _logger->createVectorVariable("qddot_value", n, 1, 10000);
-    _logger->createVectorVariable("x", n + 3 * (int)nc, 1, 10000);
+    _logger->createVectorVariable("x", n + _wd * (int)nc, 1, 10000);
     return true;
 }
 
@@ -169,7 +176,7 @@ void ForceAccExample::control_loop(double time, double period) // :167-253
     /* Retrieve values (:196-201) */
     for (int j = 0; j < n; ++j) _qddot_value[j] = _x[j];
     for (size_t i = 0; i < nc; i++) {
-        for (int k = 0; k < 3; ++k) _wrench_value[i][k] = _x[n + 3 * i + k];
+        for (int k = 0; k < _wd; ++k) _wrench_value[i][k] = _x[n + _wd * i + k];
         _logger->add(_contact_links[i] + "_wrench", _wrench_value[i]);
     }
 
@@ -177,7 +184,7 @@ void ForceAccExample::control_loop(double time, double period) // :167-253
     _tau_c.setZero(_model->getJointNum());
     for (size_t i = 0; i < nc; i++) {
         const double *Jc = _in[9].data() + i * 6 * n; // row-major 6 x n
-        for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < _wd; ++k)
             for (int j = 0; j < n; ++j) _tau_c[j] += Jc[k * n + j] * _wrench_value[i][k];
     }
     _model->setJointEffort(_tau); // :219

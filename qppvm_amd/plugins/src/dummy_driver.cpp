@@ -31,14 +31,16 @@ static std::string tick_percentiles(std::vector<double> us)
     return buf;
 }
 
-// ForceAcc in dummy mode: dump = header (n, nc, ticks), then per tick the 13 staged solver
-// input fields, the contact mask, tau, x and the status
-static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, const char *log_prefix)
+// ForceAcc in dummy mode: dump = header (n, nc, ticks, wrench_dim; mu as a double), then per tick
+// the 13 staged solver input fields, the contact mask, tau, x and the status
+static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, const char *log_prefix, int wd, double mu)
 {
     auto handle = std::make_shared<dummy::Handle>(dummy::quadruped(n));
     handle->register_model();
     XBotPlugin::ForceAccExample plugin;
     if (log_prefix) plugin.set_log_prefix(log_prefix);
+    plugin.set_wrench_dim(wd); // SURVEY 8f-2 (--wrench6, --mu)
+    plugin.set_friction(mu);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;
@@ -53,8 +55,9 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, cons
     plugin.on_start(0.0);
     const int nc = 4;
     if (f) {
-        const int hdr[3] = {n, nc, dump_ticks};
-        std::fwrite(hdr, sizeof(int), 3, f);
+        const int hdr[4] = {n, nc, dump_ticks, plugin.wrench_dim()};
+        std::fwrite(hdr, sizeof(int), 4, f);
+        std::fwrite(&mu, sizeof(double), 1, f);
     }
     double worst = 0.0, run_total = 0.0;
     std::vector<double> tick_us;
@@ -75,7 +78,7 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, cons
             const int cm = plugin.contact_mask(), st = plugin.last_status();
             std::fwrite(&cm, sizeof(int), 1, f);
             std::fwrite(plugin.tau().data(), sizeof(double), n, f);
-            std::fwrite(plugin.x().data(), sizeof(double), n + 3 * nc, f);
+            std::fwrite(plugin.x().data(), sizeof(double), (size_t)plugin.x().size(), f);
             std::fwrite(&st, sizeof(int), 1, f);
         }
         // dummy-mode kinematics with the QP's acceleration (ForceAcc.cpp:225-226)
@@ -84,10 +87,10 @@ static int run_forceacc(int ticks, int n, const char *dump, int dump_ticks, cons
     const double total = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (f) std::fclose(f);
     plugin.close();
-    std::printf("{\"config\": 0, \"plugin\": \"ForceAccExample\", \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
+    std::printf("{\"config\": 0, \"plugin\": \"ForceAccExample\", \"wrench_dim\": %d, \"mu\": %g, \"n\": %d, \"ticks\": %d, \"us_per_tick\": %.3f, "
                 "\"run_us\": %.3f, %s, \"worst_us\": %.3f, \"busy_ticks\": %d, \"solver_errors\": %d, \"sync_flags\": %d}\n",
-                n, ticks, total / ticks, run_total / ticks, tick_percentiles(tick_us).c_str(), worst, busy_ticks,
-                plugin.solver_errors(), handle->robot().last_sync());
+                plugin.wrench_dim(), mu, n, ticks, total / ticks, run_total / ticks, tick_percentiles(tick_us).c_str(), worst,
+                busy_ticks, plugin.solver_errors(), handle->robot().last_sync());
     return 0;
 }
 
@@ -96,6 +99,8 @@ int main(int argc, char **argv)
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
     bool forceacc = false, stress = false, set_ref = false, joint_limits = false;
+    int wd = 3;
+    double mu = 0.0;
     const char *log_prefix = nullptr;
     for (int k = 1; k < argc; ++k) {
         if (!std::strcmp(argv[k], "--ticks") && k + 1 < argc) ticks = std::atoi(argv[++k]);
@@ -104,13 +109,15 @@ int main(int argc, char **argv)
         else if (!std::strcmp(argv[k], "--stress")) stress = true;
         else if (!std::strcmp(argv[k], "--set-ref")) set_ref = true; // QPPVMPlugin.cpp:217-223
         else if (!std::strcmp(argv[k], "--joint-limits")) joint_limits = true; // :169-171
+        else if (!std::strcmp(argv[k], "--wrench6")) wd = 6;                   // ForceAcc.cpp:67
+        else if (!std::strcmp(argv[k], "--mu") && k + 1 < argc) mu = std::atof(argv[++k]);
         else if (!std::strcmp(argv[k], "--log") && k + 1 < argc) log_prefix = argv[++k];
         else if (!std::strcmp(argv[k], "--dump") && k + 2 < argc) {
             dump = argv[++k];
             dump_ticks = std::atoi(argv[++k]);
         }
     }
-    if (forceacc) return run_forceacc(ticks, n > 0 ? n : 30, dump, dump_ticks, log_prefix);
+    if (forceacc) return run_forceacc(ticks, n > 0 ? n : 30, dump, dump_ticks, log_prefix, wd, mu);
     if (n <= 0) n = 39;
     dummy::Params prm;
     prm.n = n;

@@ -1,7 +1,10 @@
 """Robot models for the on-GPU rigid-body dynamics (qppvm_amd/csrc/rbd.hip).
 
 ``RobotModel`` is the host description behind ``wbq_rbd_desc`` (include/wbq.h): a kinematic
-tree of revolute joints, one per link, ``parent[i] < i``. ``centauro_like()`` builds the
+tree of revolute or prismatic joints, one per link, ``parent[i] < i``; a floating base is six
+virtual joints (``with_floating_base``: x, y, z prismatic, then z, y, x revolute, massless links
+between), task frames are a link times a fixed offset (a frame on a fixed joint of the URDF).
+``qppvm_amd.urdf.load_urdf`` builds one from a URDF file. ``centauro_like()`` builds the
 synthetic stand-in for the CENTAURO model the reference loads from its URDF/YAML
 (QPPVMPlugin.cpp:50-51; not in the container): a pelvis-fixed torso joint with two 7-DoF arms
 (links ``arm1_1..7`` = 1..7, ``arm2_1..7`` = 8..14, the dof order of the dummy robot) and four
@@ -29,6 +32,9 @@ class RobotModel:
     task_link: np.ndarray    # [T] int32
     gravity: tuple = (0.0, 0.0, -9.81)
     names: list = field(default_factory=list)
+    jtype: np.ndarray | None = None        # [n] int32, 0 revolute / 1 prismatic (None: revolute)
+    task_offset: np.ndarray | None = None  # [T][12] task frame in its link's frame (None: identity)
+    task_names: list = field(default_factory=list)
 
     @property
     def n(self) -> int:
@@ -74,6 +80,32 @@ def random_tree(parent, seed=0, task_link=(), names=None, link_len=(0.08, 0.3)):
         inertia[i] = [Ib[0, 0], Ib[1, 1], Ib[2, 2], Ib[0, 1], Ib[0, 2], Ib[1, 2]]
     return RobotModel(parent=np.asarray(parent, dtype=np.int32), X_fixed=X, axis=axis, mass=mass, com=com,
                       inertia=inertia, task_link=np.asarray(task_link, dtype=np.int32), names=names or [])
+
+
+REVOLUTE, PRISMATIC = 0, 1
+
+
+def with_floating_base(model: RobotModel, base_mass: float = 20.0, base_com=(0.0, 0.0, 0.0),
+                       base_inertia=(0.6, 0.5, 0.3, 0.0, 0.0, 0.0)) -> RobotModel:
+    """The model on a floating base: six virtual joints first (translation x, y, z, then rotation
+    z, y, x about the moving axes: q[0:3] base position, q[3:6] ZYX Euler angles), the base body
+    (mass, COM, inertia in its frame) on the sixth; the model's roots hang off the base body. The
+    ForceAcc contact form's first n_fb = 6 coordinates (ForceAcc.cpp:256-282 set the base state
+    from the simulator)."""
+    n0 = model.n
+    eye = np.array([1.0, 0, 0, 0, 0, 1.0, 0, 0, 0, 0, 1.0, 0])
+    X = np.vstack([np.tile(eye, (6, 1)), model.X_fixed])
+    axis = np.vstack([np.eye(3), np.array([[0, 0, 1.0], [0, 1.0, 0], [1.0, 0, 0]]), model.axis])
+    parent = np.concatenate([np.arange(-1, 5), np.where(model.parent < 0, 5, model.parent + 6)]).astype(np.int32)
+    mass = np.concatenate([np.zeros(5), [base_mass], model.mass])
+    com = np.vstack([np.zeros((5, 3)), np.asarray(base_com, dtype=float)[None], model.com])
+    inertia = np.vstack([np.zeros((5, 6)), np.asarray(base_inertia, dtype=float)[None], model.inertia])
+    jt = np.concatenate([[PRISMATIC] * 3, [REVOLUTE] * 3,
+                         model.jtype if model.jtype is not None else np.zeros(n0, np.int32)]).astype(np.int32)
+    return RobotModel(parent=parent, X_fixed=X, axis=axis, mass=mass, com=com, inertia=inertia,
+                      task_link=np.asarray(model.task_link, np.int32) + 6, gravity=model.gravity,
+                      names=["base_x", "base_y", "base_z", "base_yaw", "base_pitch", "base_roll"] + list(model.names),
+                      jtype=jt, task_offset=model.task_offset, task_names=list(model.task_names))
 
 
 def centauro_like(seed=7) -> RobotModel:
@@ -125,7 +157,8 @@ class _Desc(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("parent", ctypes.c_void_p), ("X_fixed", ctypes.c_void_p),
                 ("axis", ctypes.c_void_p), ("mass", ctypes.c_void_p), ("com", ctypes.c_void_p),
                 ("inertia", ctypes.c_void_p), ("gravity", ctypes.c_double * 3), ("ntasks", ctypes.c_int),
-                ("task_link", ctypes.c_void_p), ("max_batch", ctypes.c_int)]
+                ("task_link", ctypes.c_void_p), ("max_batch", ctypes.c_int), ("jtype", ctypes.c_void_p),
+                ("task_offset", ctypes.c_void_p)]
 
 
 class RBDModel:
@@ -138,6 +171,9 @@ class RBDModel:
         self._keep = {k: np.ascontiguousarray(getattr(model, k),
                                               dtype=np.int32 if k in ("parent", "task_link") else np.float64)
                       for k in ("parent", "X_fixed", "axis", "mass", "com", "inertia", "task_link")}
+        for k, dt in (("jtype", np.int32), ("task_offset", np.float64)):
+            if getattr(model, k, None) is not None:
+                self._keep[k] = np.ascontiguousarray(getattr(model, k), dtype=dt)
         d = _Desc()
         d.n = model.n
         for k, v in self._keep.items():
@@ -162,6 +198,19 @@ class RBDModel:
         if rc != wbq.SUCCESS:
             raise wbq.WbqError(f"wbq_rbd_compute failed ({rc})")
         return M, h, J, pose
+
+    def compute_jdqd(self, q, qd):
+        """Host (q, qd) -> (M, h, J, pose, jdqd [B][T][6]) (wbq_rbd_compute_ex)."""
+        q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+        qd = np.ascontiguousarray(np.atleast_2d(qd), dtype=np.float64)
+        B, n, T = q.shape[0], self.model.n, self.model.ntasks
+        M = np.empty((B, n, n)); h = np.empty((B, n)); J = np.empty((B, T, 6, n)); pose = np.empty((B, T, 12))
+        jd = np.empty((B, T, 6))
+        rc = self.lib.wbq_rbd_compute_ex(self.ctx, B, q.ctypes.data, qd.ctypes.data, M.ctypes.data, h.ctypes.data,
+                                         J.ctypes.data, pose.ctypes.data, jd.ctypes.data, wbq.MEM_HOST)
+        if rc != wbq.SUCCESS:
+            raise wbq.WbqError(f"wbq_rbd_compute_ex failed ({rc})")
+        return M, h, J, pose, jd
 
     def compute_device(self, B, q_ptr, qd_ptr, M_ptr, h_ptr, J_ptr, pose_ptr):
         """Device pointers (e.g. torch tensors' data_ptr()), asynchronous on the context stream."""

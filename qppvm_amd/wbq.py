@@ -27,7 +27,7 @@ EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_s
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
            "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail", "wbq_rollout",
            "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints", "wbq_rbd_create", "wbq_rbd_compute",
-           "wbq_rbd_set_stream", "wbq_rbd_destroy", "wbq_rollout_rbd")
+           "wbq_rbd_set_stream", "wbq_rbd_destroy", "wbq_rollout_rbd", "wbq_rbd_compute_ex")
 
 
 class WbqError(RuntimeError):
@@ -126,6 +126,7 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_get_warmstart_hints.argtypes = [P, P]
     lib.wbq_rbd_create.argtypes = [P, I, ctypes.POINTER(P)]
     lib.wbq_rbd_compute.argtypes = [P, I, P, P, P, P, P, P, I]
+    lib.wbq_rbd_compute_ex.argtypes = [P, I, P, P, P, P, P, P, P, I]
     lib.wbq_rbd_set_stream.argtypes = [P, P]
     lib.wbq_rbd_destroy.argtypes = [P]
     lib.wbq_rbd_destroy.restype = None
@@ -135,7 +136,7 @@ def load_library(path: str = LIB_PATH):
               "wbq_reset_warmstart", "wbq_create_contact", "wbq_set_contact_inputs",
               "wbq_get_contact_outputs", "wbq_set_timing", "wbq_get_timing", "wbq_get_timing_detail",
               "wbq_rollout", "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints", "wbq_rbd_create",
-              "wbq_rbd_compute", "wbq_rbd_set_stream", "wbq_rollout_rbd"):
+              "wbq_rbd_compute", "wbq_rbd_set_stream", "wbq_rollout_rbd", "wbq_rbd_compute_ex"):
         getattr(lib, f).restype = I
     _lib = lib
     return lib

@@ -78,18 +78,20 @@ def contact_level0_certificate(oracle, prob, inp, b, x):
     M, h, Jw, Jc = inp["M"][b], inp["h"][b], inp["Jw"][b], inp["Jc"][b]
     cm = int(inp["cmask"][b])
     qdd, f = x[:n], x[n:]
-    tau = M @ qdd + h - sum(Jc[c, :3].T @ f[3 * c:3 * c + 3] for c in range(nc))
+    wd = getattr(prob, "wrench_dim", 3)
+    tau = M @ qdd + h - sum(Jc[c, :wd].T @ f[wd * c:wd * c + wd] for c in range(nc))
     W = np.linalg.solve(M, Jw.T)
     cols, z, lo, hi = [], [], [], []
     for j in range(6, n):
         cols.append(W[j]); z.append(tau[j])
         lo.append(prob.tau_min[j] if prob.torque_rows else -np.inf)
         hi.append(prob.tau_max[j] if prob.torque_rows else np.inf)
-    for k in range(3 * nc):
-        c, r = divmod(k, 3)
+    wlb, wub = (prob.w_lb, prob.w_ub) if hasattr(prob, "w_lb") else (prob.f_lb, prob.f_ub)
+    for k in range(wd * nc):
+        c, r = divmod(k, wd)
         on = (cm >> c) & 1
         cols.append(W.T @ Jc[c, r]); z.append(f[k])
-        lo.append(prob.f_lb[r] if on else 0.0); hi.append(prob.f_ub[r] if on else 0.0)
+        lo.append(wlb[r] if on else 0.0); hi.append(wub[r] if on else 0.0)
     A0, z, lo, hi = np.array(cols).T, np.array(z), np.array(lo), np.array(hi)
     bb = a["bw"] + W.T @ h
     w = A0.T @ (bb - A0 @ z)

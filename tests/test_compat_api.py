@@ -28,7 +28,7 @@ def _compile(body: str) -> subprocess.CompletedProcess:
 
 
 # the reference's spellings: QPPVMPlugin.cpp:44-75,203-204,217-222,256,271-287,344-353;
-# ForceAcc.cpp:36-50,61,164,181,188,196-210,249 (OpenSoT calls excluded: the wbq C ABI replaces them)
+# ForceAcc.cpp:36-50,61,74-76,164,181,188,196-210,249 (OpenSoT calls excluded: the wbq C ABI replaces them)
 REFERENCE_SNIPPET = r'''
 struct Snippet {
     XBot::RobotInterface::Ptr _robot;
@@ -107,6 +107,10 @@ struct Snippet {
         (void)fb_twist;
         _robot->setReferenceFrom(*_model, XBot::Sync::Position, XBot::Sync::Effort);
         _model->log(_matlogger, time);
+        Eigen::VectorXd wrench_ub(6), wrench_lb(6);   // ForceAcc.cpp:74-76
+        wrench_ub << 1000, 1000, 1000, 1, 1, 1;
+        wrench_lb << -1000, -1000, 10, -1, -1, -1;
+        (void)wrench_ub;
     }
 };
 '''

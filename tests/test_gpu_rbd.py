@@ -109,3 +109,82 @@ def test_rollout_rbd_matches_cpu_loop(rbd_mod, oracle_lib):
     assert rel_err(tau, tau_r) <= 1e-6, rel_err(tau, tau_r)
     assert rel_err(qd, cur["qd"]) <= 1e-9 and rel_err(q, cur["q"]) <= 1e-9
     assert np.abs(qd - qd0).max() > 1e-3  # the state moved
+
+
+def _urdf(name, tasks, fb):
+    import os
+    from qppvm_amd.urdf import load_urdf
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)
+    return load_urdf(path, task_links=tasks, floating_base=fb).model
+
+
+FEET = ["foot_fl", "foot_fr", "foot_hr", "foot_hl"]
+
+
+@pytest.mark.parametrize("name,tasks,fb", [("quadruped.urdf", ["pelvis"] + FEET, True),
+                                           ("centauro_arms.urdf", ["arm2_ee", "arm1_ee"], False)])
+def test_rbd_urdf_matches_oracle(rbd_mod, name, tasks, fb):
+    """URDF models (tests/golden/*.urdf through qppvm_amd/urdf.py): the six-joint floating base,
+    a prismatic joint, task frames behind fixed joints, and Jdot qd (wbq_rbd_compute_ex)."""
+    model = _urdf(name, tasks, fb)
+    B = 96
+    rng = np.random.default_rng(12)
+    q, qd = rng.uniform(-0.8, 0.8, (B, model.n)), rng.normal(0, 1.5, (B, model.n))
+    r = rbd_mod.RBDModel(model, max_batch=B)
+    M, h, J, pose, jd = r.compute_jdqd(q, qd)
+    r.close()
+    Mr, hr, Jr, Pr = oracle.rbd_batch(model, q, qd)
+    jdr = oracle.task_jdqd(model, q, qd)
+    assert rel_err(M, Mr) <= 1e-11, rel_err(M, Mr)
+    assert rel_err(h, hr) <= 1e-11, rel_err(h, hr)
+    assert rel_err(J.reshape(B, -1), Jr.reshape(B, -1)) <= 1e-11
+    assert rel_err(pose.reshape(B, -1), Pr.reshape(B, -1)) <= 1e-12
+    assert rel_err(jd.reshape(B, -1), jdr.reshape(B, -1)) <= 1e-11, rel_err(jd.reshape(B, -1), jdr.reshape(B, -1))
+
+
+def test_contact_rollout_rbd_matches_cpu_loop(rbd_mod, oracle_lib):
+    """ForceAcc on the device model: every step M, h, the waist (pelvis) and the four foot frames
+    (Jacobian, pose, Jdot qd) are re-evaluated from the integrated state on the floating-base URDF
+    quadruped, then the contact-form solve integrates qdd = x[0:n] (wbq_rollout_rbd) -- against the
+    oracle model + oracle contact solve + Euler on the CPU (ForceAcc.cpp:184-226)."""
+    from qppvm_amd import wbq
+    from qppvm_amd.problem import ContactProblem
+    model = _urdf("quadruped.urdf", ["pelvis"] + FEET, True)
+    B, n, nc, steps, dt = 32, model.n, 4, 8, 1e-3
+    rng = np.random.default_rng(4)
+    q0 = rng.uniform(-0.3, 0.3, (B, n))
+    q0[:, 2] += 0.6
+    qd0 = rng.normal(0, 0.3, (B, n))
+
+    def model_inputs(q, qd):
+        M, h, J, pose = oracle.rbd_batch(model, q, qd)
+        jd = oracle.task_jdqd(model, q, qd)
+        return dict(M=M, h=h, Jw=J[:, 0], jdqd_w=jd[:, 0], pose_w=pose[:, 0], Jc=np.ascontiguousarray(J[:, 1:]),
+                    jdqd_c=np.ascontiguousarray(jd[:, 1:]), pose_c=np.ascontiguousarray(pose[:, 1:]))
+    mi = model_inputs(q0, qd0)
+    pw_ref = mi["pose_w"].copy()
+    pw_ref[:, 11] -= 0.1  # ForceAcc.cpp:181: the pelvis 10 cm below its start
+    inp = dict(q=q0.copy(), qd=qd0.copy(), qref=q0.copy(), pose_w_ref=pw_ref, pose_c_ref=mi["pose_c"].copy(),
+               cmask=np.full(B, 15, np.int32), **mi)
+    prob = ContactProblem(n=n, nc=nc)
+    cur = {k: v.copy() for k, v in inp.items()}
+    for _ in range(steps):
+        cur.update(model_inputs(cur["q"], cur["qd"]))
+        tau_r, x_r, st_r, _, _ = oracle_lib.contact_batch(prob, cur)
+        qdd = x_r[:, :n].copy()
+        qdd[st_r != 0] = 0.0
+        cur["qd"] = cur["qd"] + dt * qdd
+        cur["q"] = cur["q"] + dt * cur["qd"]
+    r = rbd_mod.RBDModel(model, max_batch=B)
+    s = wbq.ContactSolver(prob, max_batch=B)
+    s.set_inputs(inp)
+    s.rollout_rbd(r, steps, dt)
+    tau, st, _ = s.outputs()
+    q, qd = s.state()
+    s.close()
+    r.close()
+    np.testing.assert_array_equal(st, st_r)
+    assert (st == 0).all()
+    assert rel_err(tau, tau_r) <= 1e-6, rel_err(tau, tau_r)
+    assert rel_err(qd, cur["qd"]) <= 1e-9 and rel_err(q, cur["q"]) <= 1e-9
+    assert np.abs(qd - qd0).max() > 1e-3

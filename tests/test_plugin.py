@@ -86,8 +86,9 @@ def test_dummy_driver_joint_limits(tmp_path, oracle_lib):
 
 def read_forceacc_dump(path):
     raw = open(path, "rb").read()
-    n, nc, ticks = (int(v) for v in np.frombuffer(raw[:12], dtype=np.int32))
-    off = 12
+    n, nc, ticks, wd = (int(v) for v in np.frombuffer(raw[:16], dtype=np.int32))
+    mu = float(np.frombuffer(raw[16:24], dtype=np.float64)[0])
+    off = 24
     shapes = {"M": (n, n), "h": (n,), "q": (n,), "qd": (n,), "qref": (n,), "Jw": (6, n), "jdqd_w": (6,),
               "pose_w": (12,), "pose_w_ref": (12,), "Jc": (nc, 6, n), "jdqd_c": (nc, 6), "pose_c": (nc, 12),
               "pose_c_ref": (nc, 12)}
@@ -99,27 +100,31 @@ def read_forceacc_dump(path):
             off += 8 * cnt
         rec["cmask"].append(int(np.frombuffer(raw[off:off + 4], dtype=np.int32)[0])); off += 4
         rec["tau"].append(np.frombuffer(raw[off:off + 8 * n], dtype=np.float64)); off += 8 * n
-        rec["x"].append(np.frombuffer(raw[off:off + 8 * (n + 3 * nc)], dtype=np.float64)); off += 8 * (n + 3 * nc)
+        rec["x"].append(np.frombuffer(raw[off:off + 8 * (n + wd * nc)], dtype=np.float64)); off += 8 * (n + wd * nc)
         rec["status"].append(int(np.frombuffer(raw[off:off + 4], dtype=np.int32)[0])); off += 4
     assert off == len(raw)
     out = {k: np.ascontiguousarray(np.array(v)) for k, v in rec.items()}
     out["cmask"] = out["cmask"].astype(np.int32)
+    out["wrench_dim"], out["mu"] = wd, mu
     return n, nc, out
 
 
-def test_forceacc_dummy_driver_matches_oracle(tmp_path, oracle_lib):
+@pytest.mark.parametrize("opts", [(), ("--wrench6", "--mu", "0.4")])
+def test_forceacc_dummy_driver_matches_oracle(tmp_path, oracle_lib, opts):
     """ForceAccExample (contact form, 4 feet, pelvis waist task) in dummy mode on the synthetic
-    floating-base quadruped: every dumped tick re-solved by the oracle's contact form."""
+    floating-base quadruped: every dumped tick re-solved by the oracle's contact form; also with
+    the full-wrench variables (ForceAcc.cpp:67 "put 6 for full wrench") and the friction pyramid."""
     from qppvm_amd import build
     from qppvm_amd.problem import ContactProblem
     driver = build.build_plugins()[1]
     dump = str(tmp_path / "dump_fa.bin")
-    r = subprocess.run([driver, "--plugin", "forceacc", "--ticks", "200", "--dump", dump, "40"],
+    r = subprocess.run([driver, "--plugin", "forceacc", "--ticks", "200", "--dump", dump, "40", *opts],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert '"plugin": "ForceAccExample"' in r.stdout
     n, nc, d = read_forceacc_dump(dump)
-    prob = ContactProblem(n=n, nc=nc)
+    assert d["wrench_dim"] == (6 if opts else 3)
+    prob = ContactProblem(n=n, nc=nc, wrench_dim=d["wrench_dim"], mu=d["mu"])
     inp = {k: d[k] for k in ("M", "h", "q", "qd", "qref", "Jw", "jdqd_w", "pose_w", "pose_w_ref", "Jc", "jdqd_c",
                              "pose_c", "pose_c_ref", "cmask")}
     tau_r, x_r, st_r, _, _ = oracle_lib.contact_batch(prob, inp)
