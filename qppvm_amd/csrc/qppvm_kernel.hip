@@ -81,6 +81,9 @@ struct FastLdsLayout {
 
 
 
+// lanes that own a joint row of a valid instance store its warm side (ws_rows exists for W1 = I)
+__device__ __forceinline__ bool go_rec(bool row, long, const QppvmArgs &a) { return row && a.ws_rows; }
+
 // Orthogonalise the normal held in NV against the rows of Q1T (two classical Gram-Schmidt
 // passes). Rows >= q of Q1T are finite and D1[c >= q] = 0, so every loop runs to NP
 // unguarded. Leaves d1 = Q1^T n in D1 and returns this lane's entry of z.
@@ -110,10 +113,18 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 // optimum) with the Q1 rows in LDS (QA rows < m0, the others zero). Pinned or equal limits
 // (lo == hi) act as equalities and are never dropped. Returns this lane's x = M u; sets
 // infeasible when no step exists (then level 0 is not attainable at b0: y* != b0).
+// Warm start (the qpOASES hot-start analogue): wsg = the side (+1 lower, -1 upper) on
+// which this lane's bound ended active in the instance's last solve. Those bounds enter the active
+// set in one batch (slot order = joint order): Gram-Schmidt of their normals against Q1, T = R^-1,
+// the step to the batch's equality-constrained optimum u += Q_W w with w = T^T r (r = the bounds'
+// residuals) and the multipliers lambda = T w. The batch is kept only if it is independent and dual
+// feasible (lambda >= 0 but on equality bounds); the loop then continues from it as from any of its
+// own states, else it starts cold. It changes the path, never the solution. With record set, the
+// final active set goes to ws_rows (status 0).
 template <int NP, int M0>
 __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u_i, int &status, int &iters,
-                                           bool &infeasible)
+                                           bool &infeasible, int wsg = 0, bool record = false)
 {
     constexpr int RS = NP + 1;
     constexpr bool MREG = ActiveLayout<NP>::MREG;
@@ -157,6 +168,83 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     const bool eqb = lo == hi;
     infeasible = false;
     __syncthreads();
+    if (__any(go && row && wsg != 0)) {
+        // ------------------------------------------------ warm start: the last active set in one batch
+        const bool wme = go && row && wsg != 0;
+        const unsigned long long bal = __ballot(wme);
+        const int base = (int)(threadIdx.x & (64 - NP)); // first lane of this instance in the wave
+        const unsigned long long mi = NP == 64 ? bal : ((bal >> base) & 0xffffffffull);
+        const int kw = __popcll(mi);
+        if (wme) S[L.BC + __popcll(mi & ((1ull << i) - 1ull))] = (double)i; // slot -> joint
+        int kwmax = kw;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) kwmax = max(kwmax, __shfl_xor(kwmax, m, 64));
+        __syncthreads();
+        const int myp = i < kw ? (int)S[L.BC + i] : 0; // this slot lane's joint
+        bool dep = false;
+        for (int a2 = 0; a2 < kwmax; ++a2) {
+            const bool on = a2 < kw;
+            const int pa = on ? __shfl(myp, a2, NP) : 0; // (project_out overwrites BC)
+            const int sa = __shfl(wsg, pa, NP);
+            const double nj = on ? sa * Mr.get(pa) : 0.0;
+            S[L.NV + i] = nj;
+            __syncthreads();
+            const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
+            const double zzr = isum<NP>(zr * zr);
+            const double npn = __shfl(nrm, pa, NP);
+            if (on && !(zzr > 1e-16 * npn * npn)) dep = true; // a dependent batch: start cold
+            double rr2 = 0.0;
+            if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
+            if (on) {
+                const double iz = zzr > 0.0 ? frsq(zzr) : 0.0;
+                S[L.QA + q * (NP + 1) + i] = zr * iz;
+                if (i < a2) Tr.set(a2, -rr2 * iz);
+                if (i == a2) Tr.set(a2, iz);
+                ++q;
+            }
+            __syncthreads();
+        }
+        // residuals r_a = beta_a - n_a . u on the slot lanes, w = T^T r (lane j: w_j), lambda = T w
+        const double s0 = Mr.dot(S + L.U, NP);
+        const double xp = __shfl(s0, myp, NP), lop = __shfl(lo, myp, NP), hip = __shfl(hi, myp, NP);
+        const int sp = __shfl(wsg, myp, NP);
+        const double r = i < kw ? (sp > 0 ? lop - xp : xp - hip) : 0.0; // sgn (bound - x)
+        double w_own = 0.0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            if (j < kwmax) {
+                const double t = isum<NP>(i < kw ? Tr.at(j) * r : 0.0);
+                w_own = i == j ? t : w_own;
+            }
+        }
+        S[L.BC + i] = i < kw ? w_own : 0.0;
+        __syncthreads();
+        const double lw = i < kw ? Tr.dot(S + L.BC, NP) : 0.0;
+        const bool peqw = __shfl(eqb ? 1 : 0, myp, NP) != 0;
+        const double lmx = imax<NP>(fabs(lw));
+        dep |= imax<NP>((i < kw && !peqw && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
+        dep = imax<NP>(dep ? 1.0 : 0.0) > 0.0; // instance-uniform
+        if (kw > 0 && !dep) { // keep: step to the batch optimum, slots take the batch
+            double du = 0.0;
+            for (int c = 0; c < kwmax; ++c)
+                if (c < kw) du = fma(S[L.QA + (m0 + c) * (NP + 1) + i], S[L.BC + c], du);
+            u_i += du;
+            if (i < kw) {
+                act_p = myp;
+                act_s = sp;
+                act_e = peqw;
+                lam = peqw ? lw : fmax(lw, 0.0);
+            }
+            k = kw;
+            iters += 1;
+        } else { // cold: drop the batch (rows of Q1 past m0 and T are rewritten before they are read)
+            Tr.zero();
+            q = m0;
+        }
+        __syncthreads();
+        S[L.U + i] = u_i;
+        __syncthreads();
+    }
     while (true) {
         const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
         if (need_select) {
@@ -280,6 +368,16 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             }
         }
     }
+    if (record) { // the final active set, by joint, for the next solve of this instance
+        S[L.NV + i] = 0.0;
+        __syncthreads();
+        if (i < k && !act_e) S[L.NV + act_p] = (double)act_s;
+        __syncthreads();
+        const double sgn = S[L.NV + i];
+        const bool ok = status == 0 && !infeasible;
+        if (go_rec(row, b, a)) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
+        __syncthreads();
+    }
     return Mr.dot(S + L.U, NP);
 }
 
@@ -315,8 +413,10 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         int status = 0, iters = 0;
         bool infeasible = false;
         WBQ_STAMP(6);
+        const bool warm_gi = valid && (a.ws_hint[b] & 2);
+        const int wsg = (warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
         const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0,
-                                            status, iters, infeasible);
+                                            status, iters, infeasible, wsg, true);
         if (infeasible) {
             if (valid && i == 0) {
                 a.status[b] = -2; // level-0 repair kernel
@@ -331,6 +431,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             if (valid && i == 0) {
                 a.status[b] = status;
                 a.iters[b] = iters;
+                a.ws_hint[b] = status == 0 ? 2 : 0; // ws_rows now holds this solve's active set
             }
         }
         WBQ_STAMP(7);
@@ -367,7 +468,7 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     const int n = a.n;
     const bool row = rep && i < n;
     const double h_i = row ? a.h[b * n + i] : 0.0;
-    const bool warm = rep && a.ws_hint[b] != 0;
+    const bool warm = rep && (a.ws_hint[b] & 1); // bit 0: the last solve went through this repair
     double lo = -kInf, hi = kInf;
     if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
     const RepairOut ro = level0_repair<NP, M0>(a, (int)(S - smem), b, i, rep, lo, hi, warm);
@@ -533,7 +634,8 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 #pragma unroll
     for (int r = 0; r < NP; ++r) A[r] = r < MR ? bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n) : 0.0;
     const double h_i = row ? h_i0 : 0.0;
-    const bool hint = valid && hint_b != 0; // the last solve needed the level-0 repair
+    const bool hint = valid && (hint_b & 1); // the last solve needed the level-0 repair
+    const bool warm_gi = valid && (hint_b & 2); // ws_rows holds its final bound active set
     S[L.QD + i] = row ? qd_i : 0.0;
 #pragma unroll
     for (int rr = 0; rr < TM * 6; ++rr)
@@ -718,7 +820,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         if (valid && i == 0) {
             a.status[b] = status;
             a.iters[b] = 0;
-            if (hint) a.ws_hint[b] = 0; // level 0 met at b0 inside the bounds
+            if (hint_b != 0) a.ws_hint[b] = 0; // level 0 met at b0 inside the bounds: no active bound
         }
     }
     if (__any(active)) {
@@ -740,7 +842,9 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
             for (int c = 0; c < NP; ++c) S[LA.QA + c * (NP + 1) + i] = (ga && c < M0 && c < m0) ? q1[c < M0 ? c : 0] : 0.0;
             int st2 = 0, it2 = 0;
             bool inf = false;
-            const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf);
+            const int wsg = (ga && warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
+            const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
+                                               true);
             const bool rep = active && (inf || to_rep);
             if (active && !rep) { // (before the repair below, which reuses the wave's LDS)
                 double tau2 = x2 + h_i;
@@ -751,6 +855,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
                 if (i == 0) {
                     a.status[b] = st2;
                     a.iters[b] = it2;
+                    a.ws_hint[b] = st2 == 0 ? 2 : 0; // ws_rows now holds this solve's active set
                 }
             }
             // the level-0 repair runs in its own kernel: inlined here its register demand spilled

@@ -348,7 +348,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              alloc_work_seen(c) && hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
              hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
              hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
-        if (ok && d.joint_weight == WBQ_WEIGHT_INERTIA) // the dual loop's warm start (dual_gi.h)
+        if (ok) // the active sets' warm start (W1 = M: dual_gi.h; W1 = I: qppvm_kernel.hip gi_solve)
             ok = hipMalloc(&c->ws_rows, B * 64) == hipSuccess && hipMemset(c->ws_rows, 0, B * 64) == hipSuccess;
         c->np = np;
         if (!ok) return cleanup(WBQ_E_DEVICE);
@@ -781,6 +781,7 @@ int wbq_get_warmstart_hints(wbq_ctx *c, uint8_t *hints)
     WBQ_HIP(hipSetDevice(c->device));
     WBQ_HIP(hipMemcpyAsync(hints, c->ws_hint, (size_t)c->batch, hipMemcpyDeviceToHost, c->stream));
     WBQ_HIP(hipStreamSynchronize(c->stream));
+    for (int b = 0; b < c->batch; ++b) hints[b] &= 1; // bit 1 (W1 = I: ws_rows valid) is internal
     return WBQ_SUCCESS;
 }
 

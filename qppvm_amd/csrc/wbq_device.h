@@ -113,6 +113,7 @@ struct RowStore<NP, true> {
         for (int j = 0; j < NP; ++j) r = (j == c) ? v[j] : r;
         return r;
     }
+    __device__ double at(int c) const { return v[c]; } // c static (after unrolling)
     __device__ double dot(const double *b, int cnt) const
     {
         double s[4] = {0.0, 0.0, 0.0, 0.0}; // four accumulators: a shorter dependent chain
@@ -133,6 +134,7 @@ struct RowStore<NP, false> {
     }
     __device__ void set(int c, double x) { row[c] = x; }
     __device__ double get(int c) const { return row[c]; }
+    __device__ double at(int c) const { return row[c]; }
     __device__ double dot(const double *b, int cnt) const
     {
         double s = 0.0;

@@ -76,12 +76,13 @@ struct QppvmArgs {
     int epoch;       // 0 / 1
     FollowGrid fg;   // follow-up grid sizing (see FollowGrid)
     // per-instance warm start across solves (the qpOASES hot-start analogue; it changes the
-    // path, never the solution): hint = the last solve needed the level-0 repair, so go there
-    // directly; state = BVLS bound state (-1/0/+1 per joint) of that repair
+    // path, never the solution): hint bit 0 = the last solve needed the level-0 repair, so go there
+    // directly; bit 1 (W1 = I) = ws_rows holds the last solve's final bound active set; state = BVLS
+    // bound state (-1/0/+1 per joint) of that repair
     unsigned char *ws_hint; // [B]
     signed char *ws_state;  // [B][NP]
-    // W1 = M: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last solve's
-    // final active set, per instance ([B][64]; dual_gi.h warm_start)
+    // the side (+1 lower / -1 upper, 0 inactive) of every constraint row (W1 = M: dual_gi.h
+    // warm_start) or torque bound (W1 = I: gi_solve) in the last solve's final active set ([B][64])
     signed char *ws_rows;
     // JointLimits toggle (include/wbq.h): the box also holds Kjl (q_min - q) - Djl qd <= tau <=
     // Kjl (q_max - q) - Djl qd ([n] each, device)

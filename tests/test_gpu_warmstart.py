@@ -91,3 +91,26 @@ def test_w1m_warm_equals_cold(wbq_mod):
         same[pick] = False
         saved += int(ic[same & ok].sum() - iw[same & ok].sum())
     assert saved > 0
+
+
+@pytest.mark.parametrize("n", [30, 39])
+def test_w1i_warm_equals_cold(wbq_mod, oracle_lib, n):
+    """W1 = I (the reference's stack): the bound active set of the last solve is added first
+    (qppvm_kernel.hip gi_solve); n = 30 runs it inline in the fast kernel, n = 39 in the active-set
+    kernel. Warm == cold to 1e-9, and == the oracle."""
+    base = QPPVMProblem(n=n)
+    inp = qppvm_instances(base, 512, seed=5)
+    alt = qppvm_instances(base, 512, seed=6)
+    s = wbq_mod.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=512)
+    tf, _, _ = s.solve_batch(inp)
+    s.close()
+    prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tf), 0.8)))
+    saved = 0
+    for k, (tw, sw, iw, tc, sc, ic, pick) in enumerate(run_churn(wbq_mod, wbq_mod.QPPVMSolver, prob, inp, alt)):
+        np.testing.assert_array_equal(sw, sc)
+        ok = sw == 0
+        assert rel_err(tw[ok], tc[ok]) <= 1e-9, rel_err(tw[ok], tc[ok])
+        same = np.ones(len(sw), bool)
+        same[pick] = False
+        saved += int(ic[same & ok].sum() - iw[same & ok].sum())
+    assert saved > 0
