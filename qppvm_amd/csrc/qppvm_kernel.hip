@@ -514,10 +514,11 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 // Level-0 repair kernel: instances with status -2 (flagged by the fast kernel, or by
 // the active-set kernel) get y* by BVLS, their pins, and a fresh dual active set. The work itself
 // is a separate (noinline) function, so the kernel's entry is only the count read, the counter
-// reset and the exit. Measured (r03, rocprofv3): an empty launch still takes ~5 us after the fast
-// kernel, with 16 blocks as with 2,048 and with or without this split, while no-work kernels with
-// the same registers / LDS / scratch / stores add ~1.7 us (scripts/launch_probe2.hip): the cost is
-// the dependent kernarg -> counter load chain after the fast kernel's input stream evicted L2.
+// reset and the exit. Measured (r03): with nothing to repair the launch adds ~1-1.5 us to a config-1
+// step (A/B with the body compiled out: 36.3 -> 35.4 us; scripts/gpu_ab_empty.sh), the launch
+// overhead of any follow-up kernel (scripts/launch_probe2.hip, launch_probe3.hip: registers, LDS,
+// scratch, kernarg size and a cold L2 do not change it); rocprofv3's ~5 us duration for it includes
+// the dispatch.
 template <int NP, int M0>
 __device__ __noinline__ void repair_list(const QppvmArgs &a, int cnt)
 {
