@@ -730,15 +730,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         for (int j = 0; j < NQ; ++j) pb.aq[j] = aq[j];
     }
     const GiVecs gv{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, SREG ? KMR + 1 : L.TS};
-    bool warm = false;
-    if constexpr (!REPAIR) { // the last solve's final active set in one batch (dual_gi.h warm_start)
-        if (gs.status == 0 && a.ws_rows) {
-            const int wsg = kind == 2 ? (int)a.ws_rows[b * 64 + i] : 0;
-            const bool iseq = kind == 1;
-            warm = warm_start<KM>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, iseq, wsg);
-        }
-    }
-    if (gs.status == 0 && !warm) {
+    if (gs.status == 0) {
         // The 12 equality rows in one batch. Lane r < 12 holds row r of Gamma_EE; a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane
         // c then forward-substitutes column c of T = L^-1 against the broadcast rows of L, and
@@ -809,6 +801,13 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
         __syncthreads();
     }
+    if constexpr (!REPAIR) { // the last solve's active inequality rows on top (dual_gi.h warm_extend)
+        if (gs.status == 0 && a.ws_rows) {
+            const int wsg = kind == 2 ? (int)a.ws_rows[b * 64 + i] : 0;
+            (void)warm_extend<KM>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, wsg);
+        }
+    }
+    WBQ_STAMP(8);
     dual_gi<KM>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs, a.max_iter);
     if (gs.status != 1 && gs.status != 3) break;
     }

@@ -296,77 +296,89 @@ __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k,
     }
 }
 
-// Warm start (the qpOASES hot-start analogue, SURVEY.md 8b ownership row): the equality rows
-// (iseq) and the inequality rows the previous solve of this instance ended with active (wsgn =
-// their side, +1 lower / -1 upper; 0 none) enter the active set in one batch -- slot order:
-// equalities, then the warm rows, each by row index. Gamma_AA is factored from scratch
-// (refactor_T), lambda_A = T^T T (b_A - s_A), and the batch is kept only if it is dual feasible
-// (every inequality multiplier >= 0, clamped at roundoff) and well conditioned (relative pivots
-// above 1e-12); the dual loop then continues from it as from any of its own states. Otherwise
-// nothing is changed and the caller starts cold. A warm start changes the path, never the
-// solution: the loop still adds every violated row and drops every blocking one.
+// Warm start on top of an existing active set (the equalities, already in the slots with their
+// multipliers and activities): the inequality rows the previous solve ended with active (wsg = their
+// side) are appended one by one with the loop's own closed-form T update (no re-factorisation), then
+// one correction of all multipliers, dlambda = T^T T (b_A - s_A) (zero residual on the rows already
+// in), makes x the optimum on the enlarged set. Kept only when every appended row is independent and
+// every inequality multiplier stays >= 0; otherwise the slots are truncated back and nothing changes.
+// It replaced a batch that re-factored the whole set from scratch (refactor_T): 52k of a 200k-cycle
+// contact-form block (profiles/r03_diag_contact.log), more than the cold path it saved. A warm start
+// changes the path, never the solution (the qpOASES hot-start analogue, SURVEY.md 8b ownership row).
 template <int KM, class P, class TrowT, class TcolT, class GAT>
-__device__ bool warm_start(const P &pb, double *S, const GiVecs &V, int i, TrowT &Trow, TcolT &Tcol, GAT &GA,
-                           int kind, double lo, double hi, double &s_i, GiState &g, bool iseq, int wsgn)
+__device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, TrowT &Trow, TcolT &Tcol, GAT &GA,
+                            int kind, double lo, double hi, double &s_i, GiState &g, int wsg)
 {
-    const bool isw = !iseq && kind == 2 && wsgn != 0;
-    const unsigned long long me = __ballot(iseq), mw = __ballot(isw);
-    const unsigned long long below = i == 0 ? 0ull : (~0ull >> (64 - i));
-    const int ne = __popcll(me), k = ne + __popcll(mw);
-    if (__popcll(mw) == 0 || k > KM || k > pb.dim) return false;
-    const int slot = iseq ? __popcll(me & below) : (isw ? ne + __popcll(mw & below) : -1);
-    if (slot >= 0) {
-        S[V.AC + slot] = (double)i;
-        S[V.WV + slot] = iseq ? 1.0 : (double)wsgn;
-    }
-    __syncthreads();
-    GiState w;
-    w.status = g.status;
-    if (i < k) {
-        w.act = (int)S[V.AC + i];
-        w.sgn = S[V.WV + i];
-        w.aeq = i < ne;
-    }
-    refactor_T(pb, S, V.TB, V.TST, i, k, w);
-    // conditioning: the relative pivot d^2 / Gamma_pp = 1 / (T_aa^2 Gamma_pp) of every slot
-    const double taa = i < k ? S[V.TB + i * V.TST + i] : 1.0;
-    const double piv = i < k ? 1.0 / (taa * taa * pb.gamma(w.act, w.act)) : kInf;
-    // (every lane takes part in every shuffle: a shuffle under a divergent branch reads lanes
-    // that did not execute it)
-    const double lo_a = __shfl(lo, w.act), hi_a = __shfl(hi, w.act), s_a = __shfl(s_i, w.act);
-    const double ye = i < k ? w.sgn * ((w.sgn > 0.0 ? lo_a : hi_a) - s_a) : 0.0;
-    S[V.VV + i] = ye;
-    Trow.load_factor(S + V.TB, V.TST, i, k, false);
-    Tcol.load_factor(S + V.TB, V.TST, i, k, true);
-    __syncthreads();
-    const double y = i < k ? Trow.dot(S + V.VV, k) : 0.0;
-    S[V.LV + i] = y;
-    __syncthreads();
-    const double lam = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
-    const double lmx = imax<64>(i < k ? fabs(lam) : 0.0);
-    const double neg = imax<64>((i < k && !w.aeq) ? -lam : 0.0);
-    if (!(-imax<64>(-piv) > 1e-12) || neg > 1e-12 * (1.0 + lmx)) {
-        Trow.zero_from(0);
-        Tcol.zero_from(0);
+    const bool isw = kind == 2 && wsg != 0 && !g.onact;
+    unsigned long long m = __ballot(isw);
+    const int k0 = g.k, kw = __popcll(m);
+    if (kw == 0 || k0 + kw > KM || k0 + kw > pb.dim) return false;
+    int k = k0;
+    bool ok = true;
+    for (int j = 0; j < kw; ++j) {
+        const int cp = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const double sgp = (double)__shfl(wsg, cp);
+        const double gpp = pb.gamma(cp, cp);
+        S[V.VV + i] = i < k ? g.sgn * sgp * pb.gamma(g.act, cp) : 0.0;
+        S[V.AC + i] = (double)g.act;
         __syncthreads();
-        return false;
+        const double l = i < k ? Trow.dot(S + V.VV, k) : 0.0;
+        S[V.LV + i] = l;
+        __syncthreads();
+        const double r = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
+        const double d2 = gpp - isum<64>(l * l);
+        if (!(d2 > P::kDep * gpp)) { // dependent on the set: no warm start
+            ok = false;
+            break;
+        }
+        const double id = frsq(d2);
+        const double tk = i < k ? -r * id : (i == k ? id : 0.0);
+        Tcol.put_dyn(k, i <= k, tk);
+        GA.put_dyn(k, kind != 0, kind != 0 ? pb.gamma(i, cp) : 0.0);
+        S[V.WV + i] = tk;
+        __syncthreads();
+        Trow.load_if(i == k, S + V.WV, k + 1);
+        if (i == k) {
+            g.act = cp;
+            g.sgn = sgp;
+            g.aeq = false;
+            g.lam = 0.0;
+        }
+        ++k;
+        __syncthreads();
     }
-    w.lam = (i < k && !w.aeq) ? fmax(lam, 0.0) : lam;
-    S[V.RV + i] = i < k ? w.sgn * w.lam : 0.0;
-    __syncthreads();
-    // activities move by Gamma[:, A] (sgn lambda); lane j keeps Gamma[j][act_q] for the loop
-#pragma unroll
-    for (int q = 0; q < KM; ++q) {
-        const int aq = __shfl(w.act, q < k ? q : 0);
-        GA.put(q, kind != 0 && q < k, kind != 0 ? pb.gamma(i, aq) : 0.0);
+    if (ok) { // dlambda = T^T T (b_A - s_A); rows already in have zero residual
+        const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act), s_a = __shfl(s_i, g.act);
+        const double res = (i >= k0 && i < k) ? g.sgn * ((g.sgn > 0.0 ? lo_a : hi_a) - s_a) : 0.0;
+        S[V.VV + i] = res;
+        S[V.AC + i] = (double)g.act;
+        __syncthreads();
+        const double y = i < k ? Trow.dot(S + V.VV, k) : 0.0;
+        S[V.LV + i] = y;
+        __syncthreads();
+        const double dl = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
+        const double lam = g.lam + dl;
+        const double lmx = imax<64>(i < k ? fabs(lam) : 0.0);
+        ok = !(imax<64>((i < k && !g.aeq && lam < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0);
+        if (ok) {
+            if (i < k) g.lam = g.aeq ? lam : fmax(lam, 0.0);
+            S[V.RV + i] = i < k ? g.sgn * dl : 0.0;
+            __syncthreads();
+            if (kind != 0) s_i += GA.dot(S + V.RV, k);
+            if (isw) g.onact = true;
+            g.k = k;
+            __syncthreads();
+            return true;
+        }
     }
-    if (kind != 0) s_i += GA.dot(S + V.RV, k);
-    w.onact = slot >= 0;
-    w.k = k;
-    w.iters = 1;
-    g = w;
+    // truncate back to the k0 slots
+    Trow.zero_if(i >= k0);
+    Tcol.zero_from(k0);
+    GA.zero_from(k0);
+    S[V.AC + i] = (double)g.act;
     __syncthreads();
-    return true;
+    return false;
 }
 
 // The side (+1 lower, -1 upper; 0 inactive or an equality slot) with which this lane's row ended

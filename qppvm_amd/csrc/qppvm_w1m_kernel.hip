@@ -307,12 +307,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     __syncthreads();
     const W1mGi pb{S, &L, m0, n, i, n};
     const GiVecs gv{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS};
-    bool warm = false;
-    if (gs.status == 0 && !R && a.ws_rows) { // level-0 rows + the last solve's active bounds in one batch
-        const int wsg = (ci >= m0 && kind == 2) ? (int)a.ws_rows[b * 64 + i] : 0;
-        warm = warm_start<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, kind == 2 && ci < m0, wsg);
-    }
-    if (gs.status == 0 && !warm) {
+    if (gs.status == 0) {
         // The m0 level-0 rows in one batch when Gamma_EE is well conditioned (dependent rows
         // are left to the loop, which never adds them): lane r < m0 holds row r of Gamma_EE, a
         // right-looking Cholesky runs across the lanes (pivots and columns by readlane), lane c
@@ -374,6 +369,11 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
             gs.iters = 1;
             __syncthreads();
         }
+    }
+    // the last solve's active bounds on top of the level-0 batch (dual_gi.h warm_extend)
+    if (gs.status == 0 && gs.k == m0 && m0 > 0 && !R && a.ws_rows) {
+        const int wsg = (ci >= m0 && kind == 2) ? (int)a.ws_rows[b * 64 + i] : 0;
+        (void)warm_extend<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, wsg);
     }
     dual_gi<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs, a.max_iter);
     __syncthreads();

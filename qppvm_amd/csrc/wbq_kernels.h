@@ -82,7 +82,7 @@ struct QppvmArgs {
     unsigned char *ws_hint; // [B]
     signed char *ws_state;  // [B][NP]
     // the side (+1 lower / -1 upper, 0 inactive) of every constraint row (W1 = M: dual_gi.h
-    // warm_start) or torque bound (W1 = I: gi_solve) in the last solve's final active set ([B][64])
+    // warm_extend) or torque bound (W1 = I: gi_solve) in the last solve's final active set ([B][64])
     signed char *ws_rows;
     // JointLimits toggle (include/wbq.h): the box also holds Kjl (q_min - q) - Djl qd <= tau <=
     // Kjl (q_max - q) - Djl qd ([n] each, device)
@@ -165,7 +165,7 @@ struct ContactArgs {
     FollowGrid fg;   // repair grid sizing (est[1]; see FollowGrid)
     int prepare;     // as QppvmArgs::prepare
     // warm start: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last
-    // solve's final active set, per instance ([B][64]; dual_gi.h warm_start)
+    // solve's final active set, per instance ([B][64]; dual_gi.h warm_extend)
     signed char *ws_rows;
 };
 
