@@ -184,7 +184,7 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
     const double *xv = S + L.XV;
     const bool jrow = ci < L.NJ, wrow = !jrow && ci < L.NJ + 6;
     const double *rq = S + (jrow ? L.AQJ + ci * L.QS : (wrow ? L.AQW + (ci - L.NJ) * L.QS : L.AQW));
-    double s = 0.0;
+    double s0 = 0.0, s1 = 0.0; // two accumulators: half the dependent FMA chain
 #pragma unroll 1
     for (int j0 = 0; j0 < NQ; j0 += 8) { // chunks of 8 independent loads (entries past n are 0)
         double rv[8], xx[8];
@@ -194,12 +194,21 @@ __device__ __forceinline__ double activity(const double *S, const ContactLayout 
             xx[u] = xv[j0 + u];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s = fma(rv[u], xx[u], s);
+        for (int u = 0; u < 8; u += 2) {
+            s0 = fma(rv[u], xx[u], s0);
+            s1 = fma(rv[u + 1], xx[u + 1], s1);
+        }
     }
+    const double s = s0 + s1;
     const double *fr = S + L.FFJ + (jrow ? ci : 0) * L.FS;
-    double sf = 0.0;
+    double sf0 = 0.0, sf1 = 0.0;
 #pragma unroll
-    for (int f = 0; f < NFM; ++f) sf = fma(f < nf ? fr[f] : 0.0, xv[n + (f < nf ? f : 0)], sf);
+    for (int f = 0; f < NFM; ++f) {
+        const double t = f < nf ? fr[f] : 0.0, xf = xv[n + (f < nf ? f : 0)];
+        if (f & 1) sf1 = fma(t, xf, sf1);
+        else sf0 = fma(t, xf, sf0);
+    }
+    const double sf = sf0 + sf1;
     if (jrow) return s + sf;
     if (wrow) return s;
     if (FR && ci >= L.NB) return fric_activity(xv + n, L, ci);
@@ -623,10 +632,12 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         for (int f = 0; f < NFM; ++f) fc[f] = f < nf ? fcoef<FR>(S, L, ci, f) : 0.0;
         for (int cl = 0; cl < ME; ++cl) {
             double g = 0.0;
-            if (cl < NJ + 6) {
+            if (cl < NJ + 6) { // four accumulators: the dot was a 32-long dependent FMA chain per entry
                 const double *xt = S + L.XT + cl * L.QS;
+                double g4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int j = 0; j < NQ; ++j) g = fma(aq[j], xt[j], g);
+                for (int j = 0; j < NQ; ++j) g4[j & 3] = fma(aq[j], xt[j], g4[j & 3]);
+                g = (g4[0] + g4[1]) + (g4[2] + g4[3]);
             }
             double gf = 0.0;
             if (cl < NJ) {

@@ -85,13 +85,14 @@ struct SlotVec<KM, true> {
     }
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
+        double s0 = 0.0, s1 = 0.0; // two accumulators: half the dependent FMA chain
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             const double bj = b[j];
-            s = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s);
+            if (j & 1) s1 = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s1);
+            else s0 = fma(j < cnt ? v[j] : 0.0, j < cnt ? bj : 0.0, s0);
         }
-        return s;
+        return s0 + s1;
     }
 };
 
@@ -134,7 +135,7 @@ struct SlotVec<KM, false> {
     }
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
+        double s = 0.0, s1 = 0.0;
         for (int c0 = 0; c0 < cnt; c0 += 8) {
             double pv[8], bv[8];
 #pragma unroll
@@ -143,9 +144,12 @@ struct SlotVec<KM, false> {
                 bv[u] = b[c0 + u];
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+            for (int u = 0; u < 8; u += 2) {
+                s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+                s1 = fma(c0 + u + 1 < cnt ? pv[u + 1] : 0.0, c0 + u + 1 < cnt ? bv[u + 1] : 0.0, s1);
+            }
         }
-        return s;
+        return s + s1;
     }
 };
 
@@ -176,7 +180,7 @@ struct TColView {
     __device__ void load_factor(const double *, int, int, int, bool) {}
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
+        double s = 0.0, s1 = 0.0;
         for (int c0 = 0; c0 < cnt; c0 += 8) {
             double pv[8], bv[8];
 #pragma unroll
@@ -185,9 +189,12 @@ struct TColView {
                 bv[u] = b[c0 + u];
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+            for (int u = 0; u < 8; u += 2) {
+                s = fma(c0 + u < cnt ? pv[u] : 0.0, c0 + u < cnt ? bv[u] : 0.0, s);
+                s1 = fma(c0 + u + 1 < cnt ? pv[u + 1] : 0.0, c0 + u + 1 < cnt ? bv[u + 1] : 0.0, s1);
+            }
         }
-        return s;
+        return s + s1;
     }
 };
 
@@ -204,7 +211,7 @@ struct GAView {
     __device__ void shift_down(int, int) {}
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
+        double s = 0.0, s1 = 0.0;
         for (int q0 = 0; q0 < cnt; q0 += 8) {
             int cq[8];
             double bv[8], gv[8];
@@ -216,9 +223,12 @@ struct GAView {
 #pragma unroll
             for (int u = 0; u < 8; ++u) gv[u] = grow[cq[u]];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s = fma(q0 + u < cnt ? gv[u] : 0.0, q0 + u < cnt ? bv[u] : 0.0, s);
+            for (int u = 0; u < 8; u += 2) {
+                s = fma(q0 + u < cnt ? gv[u] : 0.0, q0 + u < cnt ? bv[u] : 0.0, s);
+                s1 = fma(q0 + u + 1 < cnt ? gv[u + 1] : 0.0, q0 + u + 1 < cnt ? bv[u + 1] : 0.0, s1);
+            }
         }
-        return s;
+        return s + s1;
     }
 };
 
