@@ -631,9 +631,16 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     const int moff = (int)(8 * (lb * n * n + ic));
     // M is symmetric: lane i's row is its column, so row r of M read across lanes is
     // contiguous -- coalesced loads straight into the elimination registers.
-    double A[NP];
+    // (MR columns per lane: columns past MR are never pivoted and stay zero, block_gj's NC)
+    double A[MR];
+    // NP = 64: the M loads issue after the task forces. Overlapped with them, the 40 in-flight rows
+    // and the forces' temporaries exceeded the 256 VGPRs of 2 waves per SIMD, and the spill code
+    // waited on each M load in turn (vmcnt(0) per row): a serialised stage.
+    constexpr bool kForcesFirst = NP == 64;
+    if constexpr (!kForcesFirst) {
 #pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = r < MR ? bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n) : 0.0;
+        for (int r = 0; r < MR; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    }
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && (hint_b & 1); // the last solve needed the level-0 repair
     const bool warm_gi = valid && (hint_b & 2); // ws_rows holds its final bound active set
@@ -648,16 +655,20 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
         const int t = i / 6, r = i - t * 6;
-        const double xd = dot4<NP>(S + L.JR + i * NP, S + L.QD);
+        const double xd = dot4<MR>(S + L.JR + i * NP, S + L.QD);
         const double er = cart_error_component(S + L.PS + t * 24, S + L.PS + t * 24 + 12, r);
         double F = a.Kc[i] * er - a.Dc[i] * xd;
         if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
         S[L.F + i] = F;
     }
     WBQ_STAMP(15);
+    if constexpr (kForcesFirst) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+    }
     // M (still streaming in during the forces): padding rows/columns past n -> identity
 #pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+    for (int r = 0; r < MR; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
     // never has to be read again (a re-read of M would double the HBM bytes of the solve)
     double Y[M0];
@@ -667,7 +678,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         if (c < m0) {
             const int rr = a.row_sel[c];
 #pragma unroll
-            for (int j = 0; j < NP; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+            for (int j = 0; j < MR; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
         }
         Y[c] = v;
     }
@@ -686,7 +697,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
             for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
         rhs[1 + t] = c; // J_t^T F_t
     }
-    bool notspd = block_gj<NP, 1 + TM, 8>(A, rhs, n, i, S + L.PN, S + L.RH);
+    bool notspd = block_gj<NP, 1 + TM, 8, MR>(A, rhs, n, i, S + L.PN, S + L.RH);
     const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -701,7 +712,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         for (int pp = i; pp < npairs + m0; pp += NP) {
             if (pp < m0) {
                 const int rr = a.row_sel[pp], t = rr / 6;
-                S[L.RES + pp] = dot4<NP>(S + L.JR + rr * NP, S + L.WV + t * NP);
+                S[L.RES + pp] = dot4<MR>(S + L.JR + rr * NP, S + L.WV + t * NP);
             } else {
                 const int p2 = pp - m0;
                 int ra = (int)((sqrtf(8.0f * p2 + 1.0f) - 1.0f) * 0.5f);
@@ -709,7 +720,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
                 ra -= (ra * (ra + 1) / 2 > p2) ? 1 : 0;
                 const int ca = p2 - ra * (ra + 1) / 2;
                 const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
-                S[L.GR + ra * kM0Max + ca] = dot4<NP>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
+                S[L.GR + ra * kM0Max + ca] = dot4<MR>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
             }
         }
     }
@@ -806,7 +817,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         __syncthreads();
         if (active && i < m0) {
             const int rr = a.row_sel[i];
-            const double v = S[L.RES + i] + dot4<NP>(S + L.JR + rr * NP, S + L.U);
+            const double v = S[L.RES + i] + dot4<MR>(S + L.JR + rr * NP, S + L.U);
             a.b0_scr[b * kM0Max + i] = v;
         }
     }

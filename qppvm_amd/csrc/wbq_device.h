@@ -135,11 +135,22 @@ struct RowStore<NP, false> {
     __device__ void set(int c, double x) { row[c] = x; }
     __device__ double get(int c) const { return row[c]; }
     __device__ double at(int c) const { return row[c]; }
+    // chunks of 8 independent LDS reads into four accumulators instead of a chain of cnt dependent
+    // LDS round trips. Entries past cnt (up to NP) are read and masked.
     __device__ double dot(const double *b, int cnt) const
     {
-        double s = 0.0;
-        for (int j = 0; j < cnt; ++j) s = fma(row[j], b[j], s);
-        return s;
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j0 = 0; j0 < cnt; j0 += 8) {
+            double rv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                rv[u] = j0 + u < NP ? row[j0 + u] : 0.0;
+                bv[u] = j0 + u < NP ? b[j0 + u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s[u & 3] = fma(j0 + u < cnt ? rv[u] : 0.0, j0 + u < cnt ? bv[u] : 0.0, s[u & 3]);
+        }
+        return (s[0] + s[1]) + (s[2] + s[3]);
     }
 };
 
@@ -277,9 +288,13 @@ constexpr int kGjBS = 4;
 //   rows outside the block: row -= (a_i D^-1) P,   rows inside: row = (D^-1)_ri P,
 // so each row ends up normalised by its own pivot block (x_i = rhs_i, no division).
 // The next panel is updated and published first (lookahead), then the rest of the row.
-template <int NP, int NR, int RHS>
-__device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int n, int i, double *PN, double *RH)
+// NC (a multiple of BS, n <= NC <= NP): the columns held per lane. Lanes i >= NC and columns past
+// NC are identity / zero and never pivoted, so an instantiation for n <= 40 in 64 lanes carries
+// 40 columns instead of 64 (the n = 39 fast kernel: 48 fewer VGPRs, 40 % less update work).
+template <int NP, int NR, int RHS, int NC = NP>
+__device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int n, int i, double *PN, double *RH)
 {
+    static_assert(NC % kGjBS == 0 && NC <= NP, "block_gj: NC");
     constexpr int BS = kGjBS;
     bool notspd = false;
     if (i < NP) {
@@ -291,7 +306,7 @@ __device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int
         for (int m = 0; m < NR; ++m) RH[i * RHS + m] = rhs[m];
     }
 #pragma unroll
-    for (int kb = 0; kb < NP / BS; ++kb) {
+    for (int kb = 0; kb < NC / BS; ++kb) {
         const int k = kb * BS;
         if (k < n) {
             __syncthreads();
@@ -352,7 +367,7 @@ __device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int
             }
             // lookahead: next panel first
 #pragma unroll
-            for (int j = k + BS; j < k + 2 * BS && j < NP; ++j) {
+            for (int j = k + BS; j < k + 2 * BS && j < NC; ++j) {
                 double v = cc * A[j];
 #pragma unroll
                 for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
@@ -362,7 +377,7 @@ __device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int
                 if (i < NP) {
 #pragma unroll
                     for (int c = 0; c < BS; ++c)
-                        if (k + BS + c < NP) pnn[i * BS + c] = A[(k + BS + c) < NP ? k + BS + c : NP - 1];
+                        if (k + BS + c < NC) pnn[i * BS + c] = A[(k + BS + c) < NC ? k + BS + c : NC - 1];
                 }
                 const int rn = i - (k + BS);
                 if (rn >= 0 && rn < BS) {
@@ -371,7 +386,7 @@ __device__ __forceinline__ bool block_gj(double (&A)[NP], double (&rhs)[NR], int
                 }
             }
 #pragma unroll
-            for (int j = k + 2 * BS; j < NP; ++j) {
+            for (int j = k + 2 * BS; j < NC; ++j) {
                 double v = cc * A[j];
 #pragma unroll
                 for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);

@@ -225,7 +225,7 @@ public:
     // dummy-mode physics: q'' = M^-1 (tau - h), semi-implicit Euler
     void step(const Model &model, double dt)
     {
-        if (tau_.size() != (size_t)n_) return;
+        if (tau_.size() != (Eigen::Index)n_) return;
         Eigen::MatrixXd M;
         Eigen::VectorXd h;
         model.getInertiaMatrix(M);
