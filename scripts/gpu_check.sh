@@ -19,10 +19,11 @@ if [ $rc -ge 2 ]; then echo "pytest crashed/timed out ($rc): stopping"; exit $rc
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench 400 python bench.py --steps 200 --warmup 20 || exit 1
 if [ "$STEPS" = "all" ]; then
-  run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu --no-pmc --no-variant || exit 1
+  run bench_cfg2 300 python bench.py --config 2 --steps 100 --warmup 10 --no-cpu --no-variant || exit 1
   run bench_contact_cfg2 300 python bench.py --form contact --config 2 --steps 100 --warmup 10 --no-cpu || exit 1
   run bench_w1m 300 python bench.py --weight M --steps 100 --warmup 10 --no-cpu --no-variant || exit 1
-  run bench_w1m_cfg2 300 python bench.py --weight M --config 2 --steps 50 --warmup 5 --no-cpu --no-pmc --no-variant || exit 1
+  run bench_w1m_cfg2 300 python bench.py --weight M --config 2 --steps 50 --warmup 5 --no-cpu --no-variant || exit 1
+  run bench_n39 300 python bench.py --n 39 --steps 100 --warmup 10 --no-cpu --no-variant || exit 1
   run bench_cfg4 300 python bench.py --config 4 --steps 20 --warmup 2 --cpu-seconds 10 --no-variant || exit 1
   run bench_cfg4_survey 300 python bench.py --config 4 --mpc-inputs survey --steps 5 --warmup 1 --no-cpu --no-pmc --no-variant || exit 1
   cd /tmp && run_dir="$GRAFT_REPO_ROOT/gpurun_out/prof"
