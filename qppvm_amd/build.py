@@ -2,6 +2,7 @@
 the .so lives next to this file so it travels to the GPU box with the repo snapshot."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -34,11 +35,19 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
              "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
              "-I", os.path.join(ROOT, "include"),
              *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines]]
-    # one translation unit per process (each holds its own kernels), then one link
-    objs = [f"{lib}.{os.path.splitext(s)[0]}.o" for s in SOURCES]
+    # one translation unit per process (each holds its own kernels), then one link. Objects are
+    # kept per flag set; a source is recompiled only when it or a header it includes is newer
+    objdir = os.path.join(HERE, "build", "obj_" + hashlib.md5(" ".join(flags).encode()).hexdigest()[:10])
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.splitext(s)[0] + ".o") for s in SOURCES]
     procs = []
     for s, o in zip(SOURCES, objs):
-        cmd = flags + ["-c", os.path.join(CSRC, s), "-o", o]
+        src = os.path.join(CSRC, s)
+        deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "wbq.h")]
+        if not force or os.environ.get("WBQ_INCREMENTAL"):
+            if os.path.exists(o) and all(os.path.getmtime(d) <= os.path.getmtime(o) for d in deps):
+                continue
+        cmd = flags + ["-c", src, "-o", o]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd)))
@@ -46,8 +55,6 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
     subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", *objs, "-o", lib + ".tmp"])
-    for o in objs:
-        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 

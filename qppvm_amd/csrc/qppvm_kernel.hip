@@ -571,7 +571,7 @@ constexpr int kNp64OneRound = 1024;
 // MR: rows of M loaded (n <= MR, compile time; the rest of the NP padding rows are identity
 // without a load): with n = 39 and MR = 40 the stage issues ~59 loads per lane instead of ~83,
 // under the 63 outstanding vector memory operations.
-template <int NP, int M0, bool MERGED, int TM, int W, int MR>
+template <int NP, int M0, bool MERGED, int TM, int W, int MR, bool INLREP = false>
 __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -587,6 +587,9 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     const bool row = valid && i < n;
     const long bn = valid ? b * n : 0;
     const int ic = i < n ? i : n - 1; // clamped column for unconditional loads
+    // INLREP (no follow-up kernel publishes counts): the previous solve's counts, complete by
+    // stream order, for the host's choice of the next solve's variant (FollowGrid)
+    if constexpr (MERGED && INLREP) follow_publish(a.fg, a.work[(a.epoch ^ 1) * 2], a.work[(a.epoch ^ 1) * 2 + 1]);
     WBQ_RTSTAMP(16);
     WBQ_STAMP(0);
 
@@ -627,19 +630,33 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
             pv[it] = (c < 12) ? p0 : p1;
         }
     }
+    // NP = 64: the M loads issue after the task forces. Overlapped with them, the 40 in-flight rows
+    // and the forces' temporaries exceeded the 256 VGPRs of 2 waves per SIMD, and the spill code
+    // waited on each M load in turn (vmcnt(0) per row): a serialised stage.
+    constexpr bool kForcesFirst = NP == 64;
+    // NP = 32: the task-force gains of this lane's task row, loaded before M (a load issued after
+    // M and waited for in the forces would wait for all of M)
+    const int fr = i < T * 6 ? i : T * 6 - 1;
+    double Kc_i = 0.0, Dc_i = 0.0;
+    if constexpr (!kForcesFirst) {
+        Kc_i = a.Kc[fr];
+        Dc_i = a.Dc[fr];
+    }
+    // NP = 32, issue order pinned: the scheduler hoisted the M loads above the J loads and sank a
+    // J load into the uniform branch of its LDS store, where it waited with vmcnt(0) -- for all of
+    // M -- before the task forces (vmcnt retires in order). Measured (same box): n = 30 config 1
+    // 112.1 -> 114.9 M QP/s; the same pinning in the NP = 64 kernel cost 11 %
+    if constexpr (!kForcesFirst) __builtin_amdgcn_sched_barrier(0);
     const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b0, B, (long)n * n);
     const int moff = (int)(8 * (lb * n * n + ic));
     // M is symmetric: lane i's row is its column, so row r of M read across lanes is
     // contiguous -- coalesced loads straight into the elimination registers.
     // (MR columns per lane: columns past MR are never pivoted and stay zero, block_gj's NC)
     double A[MR];
-    // NP = 64: the M loads issue after the task forces. Overlapped with them, the 40 in-flight rows
-    // and the forces' temporaries exceeded the 256 VGPRs of 2 waves per SIMD, and the spill code
-    // waited on each M load in turn (vmcnt(0) per row): a serialised stage.
-    constexpr bool kForcesFirst = NP == 64;
     if constexpr (!kForcesFirst) {
 #pragma unroll
         for (int r = 0; r < MR; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+        __builtin_amdgcn_sched_barrier(0);
     }
     const double h_i = row ? h_i0 : 0.0;
     const bool hint = valid && (hint_b & 1); // the last solve needed the level-0 repair
@@ -655,10 +672,32 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
         const int t = i / 6, r = i - t * 6;
-        const double xd = dot4<MR>(S + L.JR + i * NP, S + L.QD);
-        const double er = cart_error_component(S + L.PS + t * 24, S + L.PS + t * 24 + 12, r);
-        double F = a.Kc[i] * er - a.Dc[i] * xd;
-        if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
+        // the error first, then the twist: overlapped, the twist's LDS operands and the rotation
+        // error's temporaries spilled (a scratch reload issued after M waits for all of M)
+        double er, xd;
+        if constexpr (kForcesFirst) {
+            xd = dot4<MR>(S + L.JR + i * NP, S + L.QD);
+            er = cart_error_component(S + L.PS + t * 24, S + L.PS + t * 24 + 12, r);
+        } else {
+            er = cart_error_component(S + L.PS + t * 24, S + L.PS + t * 24 + 12, r);
+            __builtin_amdgcn_sched_barrier(0);
+            xd = dot4<MR>(S + L.JR + i * NP, S + L.QD);
+        }
+        if constexpr (kForcesFirst) {
+            Kc_i = a.Kc[i];
+            Dc_i = a.Dc[i];
+        }
+        double F = Kc_i * er - Dc_i * xd;
+        // (the row masks packed into one uniform word: a per-lane indexed read of the kernel
+        // argument is a vector load, and waiting for it after M's loads waits for all of M)
+        if constexpr (kForcesFirst) {
+            if (a.select_mode == 1 && !((a.row_mask[t] >> r) & 1)) F = 0.0;
+        } else {
+            unsigned rm = 0;
+#pragma unroll
+            for (int tt = 0; tt < kTMax; ++tt) rm |= ((unsigned)a.row_mask[tt] & 63u) << (6 * tt);
+            if (a.select_mode == 1 && !((rm >> i) & 1u)) F = 0.0;
+        }
         S[L.F + i] = F;
     }
     WBQ_STAMP(15);
@@ -824,6 +863,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 
     // level-0 infeasible, or (warm start) it was last time: straight to the repair kernel
     const bool to_rep = l0bad || hint;
+    bool rep_inl = false; // INLREP: this instance's level-0 repair runs at the end of this kernel
     if (!active) {
         double tau_i = x_i + h_i;
         if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
@@ -872,7 +912,9 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
             }
             // the level-0 repair runs in its own kernel: inlined here its register demand spilled
             // into the fast path
-            if (rep && i == 0) {
+            if constexpr (INLREP) {
+                rep_inl = rep;
+            } else if (rep && i == 0) {
                 a.status[b] = -2; // qppvm_repair_kernel
                 wl_push(a, 1, b);
             }
@@ -890,6 +932,21 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         }
     }
     WBQ_STAMP(5);
+    if constexpr (MERGED && INLREP) {
+        // one launch per solve: no follow-up kernel resets the next solve's work counters
+        if (blockIdx.x == 0 && tid == 0) {
+            a.work[(a.epoch ^ 1) * 2] = 0;
+            a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+        }
+        // the level-0 repair at the kernel's top level, after every fast-path value is dead, so
+        // its register demand does not reach the fast path (inlined inside the active-set branch
+        // it spilled there)
+        if (__any(rep_inl)) {
+            if (rep_inl && i == 0) atomicAdd(a.work + a.epoch * 2 + 1, 1); // the repair count (grid policy)
+            __syncthreads();
+            repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
+        }
+    }
     WBQ_RTSTAMP(17);
 }
 
@@ -903,6 +960,9 @@ hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t str
     return hipGetLastError();
 }
 
+template <int M0>
+constexpr bool kInlineRepair = M0 <= 6;
+
 template <int NP, int M0>
 hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
@@ -913,8 +973,19 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     using Lay = FastLdsLayout<NP, MERGED>;
     hipError_t e;
     if constexpr (NP == 32) {
-        e = a.ntasks <= 2 ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 32>, a, grid, stream)
-                          : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 2, 32>, a, grid, stream);
+        // (the inline repair only where it keeps 2 waves per SIMD: M0 <= 6)
+        const bool inl = kInlineRepair<M0> && (a.inline_repair || a.prepare);
+        const bool sep = !inl || a.prepare;
+        e = hipSuccess;
+        if constexpr (kInlineRepair<M0>) {
+            if (inl)
+                e = a.ntasks <= 2
+                        ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 32, true>, a, grid, stream)
+                        : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 2, 32, true>, a, grid, stream);
+        }
+        if (e == hipSuccess && sep)
+            e = a.ntasks <= 2 ? launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, 2, 2, 32>, a, grid, stream)
+                              : launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 2, 32>, a, grid, stream);
     } else if (a.ntasks > 2) {
         e = launch_one<NP, Lay>(qppvm_fast_kernel<NP, M0, MERGED, kTMax, 1, 64>, a, grid, stream);
     } else {
@@ -937,6 +1008,7 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
         if (e != hipSuccess) return e;
     }
     // follow-up kernels: grid-stride over their work lists, grids sized from the last counts seen
+    if (MERGED && kInlineRepair<M0> && a.inline_repair && !a.prepare) return hipSuccess; // repaired in the fast kernel
     const unsigned g1 = follow_blocks(a.fg.est[1], IPW, kFollowGrid, a.B);
     if constexpr (MERGED) {
         return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -74,6 +75,7 @@ struct wbq_ctx {
     double *jl = nullptr;             // [4][n] joint-limit box: q_min, q_max, Kjl, Djl (JointLimits toggle)
     size_t np = 0;
     int epoch = 0;
+    int inl_hold = 0; // solves left in the inline-repair variant since a solve last needed a repair
     // follow-up grid sizing (wbq_kernels.h FollowGrid): counts the last follow-up kernel saw, in
     // mapped pinned host memory (device view work_seen_dev), and the host's running estimate
     int *work_seen = nullptr, *work_seen_dev = nullptr;
@@ -604,6 +606,18 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.integrate = integrate;
     a.dt = dt;
     a.prepare = prepare ? 1 : 0;
+    {
+        // n <= 32: the level-0 repair runs inside the fast kernel when the last solves needed it
+        // (one launch per solve instead of a follow-up launch that waits for the whole fast kernel:
+        // config 4 7.8 -> 9.8 M QP/s), in qppvm_repair_kernel otherwise (the inline variant's fast
+        // path is ~5 us slower than the ~3 us that launch costs: config 1). WBQ_INLREP=0/1 forces it.
+        static const int env_inl = [] { const char *e = getenv("WBQ_INLREP"); return e ? atoi(e) : -1; }();
+        // (held for 64 solves after the last repair seen: rollouts repair a few instances now and then)
+        const int seen1 = c->work_seen ? __atomic_load_n(c->work_seen + 1, __ATOMIC_RELAXED) : 0;
+        if (seen1 > 0) c->inl_hold = 64;
+        else if (c->inl_hold > 0) --c->inl_hold;
+        a.inline_repair = env_inl >= 0 ? env_inl : (c->inl_hold > 0 ? 1 : 0);
+    }
 
     WBQ_HIP(hipSetDevice(c->device));
     if (prepare) {

@@ -96,6 +96,9 @@ struct QppvmArgs {
     // launch (any batch size) and launches nothing. wbq_create does this once, so a solve takes no
     // lock and never allocates (include/wbq.h: wbq_solve is RT-safe)
     int prepare;
+    // NP = 32: the level-0 repair runs at the end of the fast kernel (one launch per solve) instead
+    // of in qppvm_repair_kernel
+    int inline_repair;
 };
 
 // The box on x = tau - h of joint j (QPPVMPlugin.cpp:203-205: tau limits shifted by -h; with the

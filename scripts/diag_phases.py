@@ -29,7 +29,7 @@ def run(libpath, prob, inp, reps=20, stamps=False):
     out = {"us_per_launch": 1e3 * ms / cnt}
     if stamps:
         B = inp["h"].shape[0]
-        nb = B if (prob.n > 32 or os.environ.get("WBQ_MFMA_MAX_BATCH", "1") != "0") else (B + 1) // 2
+        nb = B if prob.n > 32 else (B + 1) // 2  # blocks of the fast kernel: 2 instances per wave for n <= 32
         K = 20
         buf = (ctypes.c_ulonglong * (K * nb))()
         s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
