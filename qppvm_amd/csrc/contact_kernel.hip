@@ -455,8 +455,13 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     const int voff = (int)(8 * ic);
     const double q_i = bload(rsrc_at(a.q, b, B, n), voff, 0), qd_i = bload(rsrc_at(a.qd, b, B, n), voff, 0);
     const double qref_i = bload(rsrc_at(a.qref, b, B, n), voff, 0), h_i0 = bload(rsrc_at(a.h, b, B, n), voff, 0);
+    // torque-row variants: M last, its issue order pinned (vmcnt retires in order), so the task
+    // targets and H (steps 2-3, no M) run while M streams in, and M enters LDS only before the
+    // elimination reads it. Same box: config 2 (torque rows) 5.80 -> 6.17 M QP/s, the variant's
+    // spill gone; the register-slot variants lost 4-8 % with it (M live through steps 2-3)
+    constexpr bool kMLate = TR;
     double mrow[NQ]; // M is symmetric: lane i's row is its column, so the loads coalesce
-    {
+    if constexpr (!kMLate) {
         const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
         const int moff = (int)(8 * ic);
 #pragma unroll
@@ -485,16 +490,24 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     }
     double jd = 0.0;
     if (i < 6 * (1 + nc)) jd = i < 6 ? a.jdqd_w[b * 6 + i] : a.jdqd_c[b * nc * 6 + i - 6];
-    const double h_i = qrow ? h_i0 : 0.0;
+    if constexpr (kMLate) {
+        __builtin_amdgcn_sched_barrier(0);
+        const __amdgpu_buffer_rsrc_t Mrs = rsrc_at(a.M, b, B, (long)n * n);
+        const int moff = (int)(8 * ic);
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) mrow[r] = (qrow && r < n) ? mrow[r] : 0.0;
+        for (int r = 0; r < NQ; ++r) mrow[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const double h_i = qrow ? h_i0 : 0.0;
 #pragma unroll
     for (int rr = 0; rr < 6 * CM; ++rr) jc[rr] = (qrow && rr < 6 * nc) ? jc[rr] : 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) jw[r] = qrow ? jw[r] : 0.0;
     if (i < L.NJ) { // joint constraint rows (every joint with torque rows, else the 6 base rows)
+        if constexpr (!kMLate) {
 #pragma unroll
-        for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = mrow[r];
+            for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = (qrow && r < n) ? mrow[r] : 0.0;
+        }
 #pragma unroll
         for (int f = 0; f < NFM; ++f)
             if (f < nf) S[L.FFJ + i * L.FS + f] = ((cm >> (f / WD)) & 1) ? -jc[6 * (f / WD) + f % WD] : 0.0;
@@ -511,7 +524,8 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     for (int it = 0; it < kPoseIt; ++it)
         if (it * 64 + i < 24 * (1 + nc)) S[L.PS + it * 64 + i] = pv[it];
     if (i < 6 * (1 + nc)) S[L.JD + i] = jd;
-    __syncthreads();
+    if constexpr (kMLate) lds_barrier(); // (LDS only: M keeps streaming in)
+    else __syncthreads();
     WBQ_STAMP(1);
 
     // ------------------------------------------------- 2. task targets (one lane per row)
@@ -525,7 +539,8 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         const double Kp = t == 0 ? a.Kp_w : a.Kp_f, Kd = t == 0 ? a.Kd_w : a.Kd_f;
         S[L.BT + i] = Kp * e - Kd * xd - S[L.JD + i];
     }
-    __syncthreads();
+    if constexpr (kMLate) lds_barrier();
+    else __syncthreads();
 
     // ------------------------------- 3. H row i = e_i + sum_c J_c^T J_c row i, gradient
     double A[NQ];
@@ -547,6 +562,13 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         for (int j = 0; j < NQ; ++j) S[L.HR + i * L.QS + j] = A[j];
     }
 
+    if constexpr (kMLate) { // the joint constraint rows' M part (M arrives here)
+        if (i < L.NJ) {
+#pragma unroll
+            for (int r = 0; r < NQ; ++r) S[L.AQJ + i * L.QS + r] = (qrow && r < n) ? mrow[r] : 0.0;
+        }
+        lds_barrier();
+    }
     WBQ_STAMP(2);
     // ------------- 4. X = H_qq^-1 [M rows 0..NJ-1 | J_w^T | -g]: block Gauss-Jordan, H SPD
     bool notspd = false;
