@@ -12,16 +12,57 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwbq.so")
 SOURCES = ["wbq_api.hip", "qppvm_kernel.hip", "qppvm_w1m_kernel.hip", "contact_kernel.hip", "rbd.hip"]
-HEADERS = ["wbq_kernels.h", "wbq_device.h", "dual_gi.h", "qppvm_repair.h"]
 ARCH = os.environ.get("WBQ_ARCH", "gfx950")
 
 
+def _headers(src: str | None = None) -> list:
+    """The local headers a translation unit includes, followed recursively through its
+    #include "..." lines (src None: every csrc/*.h), and the C ABI header."""
+    inc = [os.path.join(ROOT, "include", "wbq.h")]
+    if src is None:
+        return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")) + inc
+    seen, todo = [], [src]
+    while todo:
+        with open(todo.pop()) as f:
+            for line in f:
+                line = line.strip()
+                if line.startswith("#include \""):
+                    h = os.path.join(CSRC, line.split('"')[1])
+                    if os.path.exists(h) and h not in seen:
+                        seen.append(h)
+                        todo.append(h)
+    return sorted(seen) + inc
+
+
+def _digest(flags: list, paths: list) -> str:
+    """Content hash of the compile flags and the files (not their modification times: a copied
+    tree with reset timestamps must not relink stale objects)."""
+    h = hashlib.sha256(" ".join(flags).encode())
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _stamp(lib: str) -> str:
+    return lib + ".srchash"
+
+
 def _stale() -> bool:
+    """The product library is stale when the content hash of its sources differs from the one
+    recorded beside it at link time (no record: fall back to modification times)."""
     if not os.path.exists(LIB):
         return True
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + _headers()
+    if os.path.exists(_stamp(LIB)):
+        with open(_stamp(LIB)) as f:
+            return f.read().strip() != _digest(_FLAGS_KEY, deps)
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "wbq.h")]
     return any(os.path.getmtime(p) > t for p in deps)
+
+
+_FLAGS_KEY = ["product", ARCH]
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False, defines: tuple = (),
@@ -35,27 +76,34 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
              "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
              "-I", os.path.join(ROOT, "include"),
              *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines]]
-    # one translation unit per process (each holds its own kernels), then one link. Objects are
-    # kept per flag set; a source is recompiled only when it or a header it includes is newer
-    objdir = os.path.join(HERE, "build", "obj_" + hashlib.md5(" ".join(flags).encode()).hexdigest()[:10])
+    # one translation unit per process (each holds its own kernels), then one link. An object is
+    # keyed by the content hash of its flags, its source and every header, so it is reused only
+    # when none of them changed (WBQ_INCREMENTAL=1 reuses objects on a forced build too)
+    objdir = os.path.join(HERE, "build", "obj")
     os.makedirs(objdir, exist_ok=True)
-    objs = [os.path.join(objdir, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    hdrs = _headers()
+    objs = [os.path.join(objdir, os.path.splitext(s)[0] + "_" +
+                         _digest(flags, [os.path.join(CSRC, s)] + _headers(os.path.join(CSRC, s))) + ".o")
+            for s in SOURCES]
     procs = []
     for s, o in zip(SOURCES, objs):
         src = os.path.join(CSRC, s)
-        deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "wbq.h")]
-        if not force or os.environ.get("WBQ_INCREMENTAL"):
-            if os.path.exists(o) and all(os.path.getmtime(d) <= os.path.getmtime(o) for d in deps):
-                continue
-        cmd = flags + ["-c", src, "-o", o]
+        if (not force or os.environ.get("WBQ_INCREMENTAL")) and os.path.exists(o):
+            continue
+        cmd = flags + ["-c", src, "-o", o + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd)))
     failed = [c for c, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
+    for c, _ in procs:
+        os.replace(c[-1], c[-1][:-4])
     subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", *objs, "-o", lib + ".tmp"])
     os.replace(lib + ".tmp", lib)
+    if lib == LIB and not defines:
+        with open(_stamp(LIB), "w") as f:
+            f.write(_digest(_FLAGS_KEY, [os.path.join(CSRC, s) for s in SOURCES] + hdrs) + "\n")
     return lib
 
 

@@ -40,6 +40,7 @@
 #include "wbq_device.h"
 #include "dual_gi.h"
 #include "qppvm_repair.h"
+#include "fric_lsi.h"
 
 #include <type_traits>
 
@@ -300,13 +301,15 @@ __device__ __forceinline__ int eq_row(int a, int NJ) { return a < 6 ? a : NJ + a
 // along the unpinned columns, so only a pivot basis of their span (wkeep: a mask of waist rows,
 // from a pivoted Cholesky of their Gram) is kept as level-1 rows -- the others are implied, and
 // keeping them makes the final active set exactly singular.
-// Friction rows (mu > 0) are not boxes in z: the BVLS runs on the box alone and the level-0 point
-// is accepted only if it meets every friction face; otherwise the instance ends with status 2
-// (fricbad: the GPU repair does not solve level 0 over the friction pyramid).
-// Updates this lane's row limits (lo, hi); returns the BVLS iterations, capped = BVLS hit its cap.
-template <int NQ>
+// Friction rows (mu > 0, FR instantiations) are general rows in z: level 0 is then an LSI over the
+// box and the pyramid faces (fric_lsi.h, BVLS generalised to the faces; the oracle keeps the friction
+// rows in its level-0 QP, oracle/wbq_oracle_contact.c:413-447), and the faces its multipliers hold
+// are pinned as equalities of level 1 like the box sides. (Until round 4 the BVLS ran on the box
+// alone and an instance whose level-0 point violated a face ended with status 2)
+// Updates this lane's row limits (lo, hi); returns the level-0 iterations, capped = the cap ended it.
+template <int NQ, bool FR>
 __device__ int contact_level0(const ContactArgs &a, long b, double *S, const ContactLayout &L, int i, double h_i,
-                              double &lo, double &hi, bool &capped, bool &fricbad, int &wkeep)
+                              double &lo, double &hi, bool &capped, int &wkeep)
 {
     const int n = a.n, nc = a.nc, wd = L.WD, nf = L.NF, na = n - 6;
     const bool qrow = i < n;
@@ -371,35 +374,51 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
         zhi = on ? fu : 0.0;
     }
     const bool row = tvar || fvar;
-    const BvlsOut bz = bvls<64, 6>(acol, bv, 6, zlo, zhi, row, true, 0, 50 * (na + nf) + 100);
-    fricbad = false;
-    if (a.nfr > 0) { // the friction faces at z* (lane NB + r: face r & 3 of contact r >> 2)
-        const int r = (i >= L.NB && i < L.ME) ? i - L.NB : 0, c = r >> 2, k = r & 3;
-        const double fx = __shfl(bz.xv, na + wd * c), fy = __shfl(bz.xv, na + wd * c + 1);
-        const double fz = __shfl(bz.xv, na + wd * c + 2);
-        const double v = ((k & 1) ? -1.0 : 1.0) * (k < 2 ? fx : fy) - L.MU * fz;
-        const bool on = (a.cmask[b] >> c) & 1;
-        const double tol = 1e-9 * fmax(1.0, fabs(fz));
-        fricbad = imax<64>((i >= L.NB && i < L.ME && on && v > tol) ? 1.0 : 0.0) > 0.0;
-    }
-    double ys[6], abm = 0.0, g = 0.0;
+    const int maxit = 50 * (na + nf) + 100;
+    double xz, mcol[6]; // z_i; the part of this lane's column level 1 can still move along
+    int pin, pfm = 0, itz;
+    bool capz;
+    if (FR && a.nfr > 0) { // box + pyramid faces: the friction groups are the active contacts' forces
+        const int fc = fvar ? f / wd : 0, fk = fvar ? f - wd * fc : 3;
+        const bool on = (a.cmask[b] >> fc) & 1;
+        const int gb = (fvar && fk < 3 && on) ? na + wd * fc : -1;
+        const LsiOut lz = fric_lsi<64, 6>(acol, bv, 6, zlo, zhi, row, gb, L.MU, maxit);
+        xz = lz.xv;
+        pin = lz.pin;
+        pfm = lz.pfm;
+        itz = lz.it;
+        capz = lz.capped;
 #pragma unroll
-    for (int r = 0; r < 6; ++r) ys[r] = isum<64>(row ? acol[r] * bz.xv : 0.0);
+        for (int r = 0; r < 6; ++r) mcol[r] = lz.mcol[r];
+    } else {
+        const BvlsOut bz = bvls<64, 6>(acol, bv, 6, zlo, zhi, row, true, 0, maxit);
+        xz = bz.xv;
+        itz = bz.it;
+        capz = bz.capped;
+        double g = 0.0, abm = 0.0, yv[6];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        abm = fma(acol[r], bv[r], abm);
-        g = fma(acol[r], bv[r] - ys[r], g);
+        for (int r = 0; r < 6; ++r) yv[r] = isum<64>(row ? acol[r] * xz : 0.0);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            abm = fma(acol[r], bv[r], abm);
+            g = fma(acol[r], bv[r] - yv[r], g);
+        }
+        abm = fmax(1.0, imax<64>(row ? fabs(abm) : 0.0));
+        pin = (row && g > 1e-9 * abm) ? 1 : ((row && g < -1e-9 * abm) ? -1 : 0);
+        const bool mov = row && pin == 0 && zlo != zhi; // columns y can still move along
+#pragma unroll
+        for (int r = 0; r < 6; ++r) mcol[r] = mov ? acol[r] : 0.0;
     }
-    abm = fmax(1.0, imax<64>(row ? fabs(abm) : 0.0));
-    const int pin = (row && g > 1e-9 * abm) ? 1 : ((row && g < -1e-9 * abm) ? -1 : 0);
+    double ys[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ys[r] = isum<64>(row ? acol[r] * xz : 0.0);
     {
         constexpr int NT = 21;
-        const bool mov = row && pin == 0 && zlo != zhi; // columns y can still move along
         double gu[NT];
 #pragma unroll
         for (int p = 0; p < 6; ++p)
 #pragma unroll
-            for (int c = 0; c <= p; ++c) gu[tri(p, c)] = mov ? acol[p] * acol[c] : 0.0;
+            for (int c = 0; c <= p; ++c) gu[tri(p, c)] = acol[p] * mcol[c];
         isum_vec<64, NT>(gu);
         PivChol<6> pc;
         pc.factor(gu, 6, 1e-10);
@@ -413,14 +432,20 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
     const int pin_c = __shfl(pin, trow ? ci - 6 : (frow ? na + ci - L.NJ - 6 : 0));
     if ((trow || frow) && pin_c > 0) lo = hi; // held at the upper limit
     if ((trow || frow) && pin_c < 0) hi = lo; // held at the lower limit
+    if (FR && a.nfr > 0) { // friction face r & 3 of contact r >> 2: held at 0 by a positive multiplier
+        const bool fface = ci >= L.NB && ci < L.ME;
+        const int r = fface ? ci - L.NB : 0;
+        const int pf = __shfl(pfm, na + wd * (r >> 2));
+        if (fface && ((pf >> (r & 3)) & 1)) lo = hi;
+    }
     if (ci >= L.NJ && ci < L.NJ + 6) {
         double y = 0.0;
 #pragma unroll
         for (int r = 0; r < 6; ++r) y = (ci - L.NJ == r) ? ys[r] - hw[r] : y;
         lo = hi = y; // the waist rows keep the level-0 optimum y0*
     }
-    capped = bz.capped;
-    return bz.it;
+    capped = capz;
+    return itz;
 }
 
 // The whole solve of instance b by one wave (lane i = threadIdx.x). REPAIR (the follow-up
@@ -689,13 +714,13 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
     WBQ_STAMP(4);
     int it0 = 0;
-    bool l0cap = false, l0fric = false;
+    bool l0cap = false;
     int wkeep = 0x3f; // waist rows kept as level-1 rows (all, except after a level-0 repair)
     const double lo_free = lo, hi_free = hi, s_x0 = s_i; // (a repair retry restarts from these)
     const int kind_free = kind;
     (void)kind_free;
     if constexpr (REPAIR) { // level 0 not attainable at b_w: y0* and the pins first
-        if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ>(a, b, S, L, i, h_i, lo, hi, l0cap, l0fric, wkeep);
+        if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ, FR>(a, b, S, L, i, h_i, lo, hi, l0cap, wkeep);
         __syncthreads();
     }
 
@@ -752,7 +777,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     Tcol.zero_from(0);
     GA.zero_from(0);
     gs = GiState();
-    gs.status = notspd ? 3 : (a.limits_crossed || l0fric ? 2 : (l0cap ? 1 : 0));
+    gs.status = notspd ? 3 : (a.limits_crossed ? 2 : (l0cap ? 1 : 0));
     // rank cap of the loop: the rows never touch the forces of inactive contacts (their rows
     // are disabled, their joint-row coefficients zero), so the rows span at most
     // n + WD * (active contacts) dimensions, not nx

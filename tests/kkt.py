@@ -66,13 +66,11 @@ def qppvm_certificate(oracle, prob, inp, b, tau):
     return dict(primal=primal, level0=level0, stat=stat, sign=sign, indep=bool(indep))
 
 
-def contact_level0_certificate(oracle, prob, inp, b, x):
-    """Level-0 optimality of a contact-form output whose waist row is not at b_w (level 0 not
-    attainable): with tau = M qdd + h - J_c^T [f; 0] every row is a box in z = (tau_a, f) and the
-    waist value is y = A0 z - J_w M^-1 h (qppvm_amd/csrc/contact_kernel.hip:contact_level0), so z
-    must solve min 0.5 ||A0 z - (b_w + J_w M^-1 h)||^2 over the box: the gradient w = A0^T (b - A0 z)
-    vanishes on interior variables, w <= 0 at lower and w >= 0 at upper bounds. Returns the scaled
-    worst violation and y."""
+def contact_level0_zspace(oracle, prob, inp, b, x):
+    """Level 0 of the contact form in z = (tau_a, w) space (qppvm_amd/csrc/contact_kernel.hip:
+    contact_level0): with tau = M qdd + h - J_c^T w every row is a box in z (plus the friction faces
+    on the forces) and the waist value is y = A0 z - J_w M^-1 h. Returns (A0, b, z, lo, hi, y) for
+    the output x = [qdd; w]."""
     a = oracle.contact_assemble(prob, inp, b)
     n, nc = prob.n, prob.nc
     M, h, Jw, Jc = inp["M"][b], inp["h"][b], inp["Jw"][b], inp["Jc"][b]
@@ -92,15 +90,63 @@ def contact_level0_certificate(oracle, prob, inp, b, x):
         on = (cm >> c) & 1
         cols.append(W.T @ Jc[c, r]); z.append(f[k])
         lo.append(wlb[r] if on else 0.0); hi.append(wub[r] if on else 0.0)
-    A0, z, lo, hi = np.array(cols).T, np.array(z), np.array(lo), np.array(hi)
-    bb = a["bw"] + W.T @ h
+    return (np.array(cols).T, a["bw"] + W.T @ h, np.array(z), np.array(lo), np.array(hi), Jw @ qdd)
+
+
+def lsi_certificate(A0, bb, z, lo, hi, groups=(), mu=0.0, act_tol=1e-8):
+    """Scaled KKT violation of z for min 0.5 ||A0 z - bb||^2 over lo <= z <= hi and, for every
+    friction group (start index j of an active contact's (f_x, f_y, f_z)), the pyramid faces
+    s f_x - mu f_z <= 0, s f_y - mu f_z <= 0: w = A0^T (bb - A0 z) (= -gradient) vanishes on free
+    variables, has the sign of the outward normal at an active bound, and on a group is a
+    non-negative combination of the outward normals of its active box sides and faces (NNLS)."""
     w = A0.T @ (bb - A0 @ z)
     scale = np.abs(A0.T).sum(axis=1) * (np.abs(A0 @ z).max() + np.abs(bb).max()) + 1e-300
-    at_lo, at_hi = _active(z, lo, hi, 1e-8)
+    at_lo, at_hi = _active(z, lo, hi, act_tol)
     v = np.where(~(at_lo | at_hi), np.abs(w), 0.0)
     v = np.maximum(v, np.where(at_lo & ~at_hi, np.maximum(w, 0.0), 0.0))
     v = np.maximum(v, np.where(at_hi & ~at_lo, np.maximum(-w, 0.0), 0.0))
-    return float((v / scale).max()), Jw @ qdd
+    primal = max(0.0, (lo - z).max(initial=0.0), (z - hi).max(initial=0.0))
+    for j in groups:
+        from scipy.optimize import nnls
+        fv, wc = z[j:j + 3], w[j:j + 3]
+        nrm, tol = [], act_tol * (1.0 + np.abs(fv).max())
+        for k in range(3):
+            e = np.zeros(3)
+            e[k] = 1.0
+            if at_lo[j + k] and not at_hi[j + k]:
+                nrm.append(-e)
+            if at_hi[j + k] and not at_lo[j + k]:
+                nrm.append(e)
+        for f in range(4):
+            nv = np.zeros(3)
+            nv[f >> 1] = -1.0 if f & 1 else 1.0
+            nv[2] = -mu
+            ph = nv @ fv
+            primal = max(primal, ph / (1.0 + np.abs(fv).max()))
+            if ph >= -tol:
+                nrm.append(nv)
+        res = nnls(np.array(nrm).T, wc)[1] if nrm else np.linalg.norm(wc)
+        sc = np.abs(scale[j:j + 3]).max()
+        v[j:j + 3] = 0.0
+        v[j] = res * scale[j] / sc
+    return float(max((v / scale).max(), primal))
+
+
+def contact_friction_groups(prob, inp, b):
+    """z-space start indices of the active contacts' force triples (friction groups; none without mu)"""
+    if float(getattr(prob, "mu", 0.0)) <= 0.0:
+        return []
+    wd, cm = getattr(prob, "wrench_dim", 3), int(inp["cmask"][b])
+    return [prob.n - 6 + wd * c for c in range(prob.nc) if (cm >> c) & 1]
+
+
+def contact_level0_certificate(oracle, prob, inp, b, x):
+    """Level-0 optimality of a contact-form output whose waist row is not at b_w (level 0 not
+    attainable): z must solve the level-0 LSI (lsi_certificate; the box, and with mu > 0 the friction
+    pyramid faces). Returns the scaled worst violation and y."""
+    A0, bb, z, lo, hi, y = contact_level0_zspace(oracle, prob, inp, b, x)
+    return lsi_certificate(A0, bb, z, lo, hi, contact_friction_groups(prob, inp, b),
+                           float(getattr(prob, "mu", 0.0))), y
 
 
 def contact_certificate(oracle, prob, inp, b, x, waist=None):

@@ -10,7 +10,7 @@ import pytest
 from conftest import load_golden_contact, rel_err
 from qppvm_amd.problem import ContactProblem
 from qppvm_amd.synth import contact_instances, replicate
-from test_gpu_contact import MASKS4, TOL, check_against_oracle, gpu_solve
+from test_gpu_contact import MASKS4, MAX_MISS, TOL, check_against_oracle, gpu_solve
 
 pytestmark = pytest.mark.gpu
 
@@ -72,3 +72,44 @@ def test_contact_ext_config1_identical(wbq_mod, oracle_lib):
     inp = replicate(contact_instances(prob, 1, seed=0), 64)
     tau, x, st, _ = check_against_oracle(wbq_mod, oracle_lib, prob, inp, min_ok=64)
     assert np.abs(tau - tau[0]).max() == 0.0
+
+
+@pytest.mark.parametrize("mu", [0.3, 0.5])
+def test_contact_level0_repair_friction(wbq_mod, oracle_lib, mu):
+    """Level 0 not attainable with the friction pyramid on (the reference's stack
+    waist / (postural + feet), ForceAcc.cpp:131-137, keeps the waist at its level-0 optimum under
+    every constraint): the GPU solves level 0 over the box AND the pyramid faces (fric_lsi.h, an LSI
+    in the BVLS pattern) as the oracle's level-0 QP does (oracle/wbq_oracle_contact.c:413-447), and
+    level 1 holds the faces and box sides its multipliers pin. The test_contact_level0_repair sweep
+    (n = 12, nc = 4, torque rows at the 40 % quantile, 20 seeds, 1,280 instances) with the cone on:
+    every instance the oracle solves, the GPU solves with the oracle's tau (MAX_MISS = 0); where the
+    oracle fails, a GPU solution carries the level-0 (LSI) and level-1 KKT certificates. Until
+    round 4 the GPU gave up with status 2 whenever the box-only level-0 point violated a face."""
+    import kkt
+    n, nc = 12, 4
+    tot = dict(solved=0, repaired=0, miss=0, extra=0)
+    for seed in range(100, 120):
+        free = ContactProblem(n=n, nc=nc, mu=mu)
+        inp = contact_instances(free, 64, seed=seed, masks=MASKS4)
+        tau_free = oracle_lib.contact_batch(free, inp)[0]
+        prob = ContactProblem(n=n, nc=nc, mu=mu, torque_rows=True,
+                              tau_max=float(np.quantile(np.abs(tau_free[:, 6:]), 0.4)))
+        tau_r, x_r, st_r, _, rep = oracle_lib.contact_batch(prob, inp)
+        tau, x, st, it = gpu_solve(wbq_mod, prob, inp)
+        solved = st_r == 0
+        tot["solved"] += int(solved.sum())
+        tot["repaired"] += int((solved & (rep != 0)).sum())
+        ok = solved & (st == 0)
+        assert rel_err(tau[ok], tau_r[ok]) <= TOL, (seed, rel_err(tau[ok], tau_r[ok]))
+        tot["miss"] += int((solved & (st != 0)).sum())
+        np.testing.assert_array_equal(tau[st != 0], inp["h"][st != 0])
+        w = x[:, n:].reshape(-1, nc, 3)
+        act = ((inp["cmask"][:, None] >> np.arange(nc)[None]) & 1).astype(bool) & (st == 0)[:, None]
+        assert np.all(np.abs(w[act][:, :2]) <= mu * w[act][:, 2:3] + 1e-8)
+        for b in np.where(~solved & (st == 0))[0]:
+            tot["extra"] += 1
+            l0, y = kkt.contact_level0_certificate(oracle_lib, prob, inp, b, x[b])
+            c = kkt.contact_certificate(oracle_lib, prob, inp, b, x[b], waist=y)
+            assert l0 <= 1e-9 and max(c["primal"], c["stat"], c["sign"]) <= 1e-9, (seed, b, l0, c)
+    assert tot["repaired"] >= 500, tot  # the friction-aware repair path really runs
+    assert tot["miss"] <= MAX_MISS, tot

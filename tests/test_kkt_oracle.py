@@ -42,3 +42,34 @@ def test_contact_certificate_accepts_oracle_and_rejects_perturbed(oracle_lib):
     assert max(ok.values()) <= TOL, ok
     bad = [kkt.contact_certificate(oracle_lib, prob, inp, b, x[b] * (1 + 1e-6)) for b in range(8)]
     assert all(max(c["primal"], c["stat"]) > 1e-9 for c in bad)
+
+
+@pytest.mark.parametrize("mu", [0.3, 0.5])
+def test_friction_lsi_certificate_and_reference(oracle_lib, mu):
+    """The level-0 LSI over the box and the friction pyramid (kernel: qppvm_amd/csrc/fric_lsi.h) as
+    its numpy statement (tests/fric_lsi_ref.py) solves it: the certificate (kkt.lsi_certificate)
+    accepts those points and rejects perturbed ones, and the waist value y0* agrees with the
+    oracle's level-0 QP (a 1e-10 ridge, oracle/wbq_oracle_contact.c) to 1e-6 relative."""
+    import fric_lsi_ref as ref
+    n, nc = 12, 4
+    free = ContactProblem(n=n, nc=nc, mu=mu)
+    inp = contact_instances(free, 64, seed=101, masks=ref.MASKS4)
+    tf = oracle_lib.contact_batch(free, inp)[0]
+    prob = ContactProblem(n=n, nc=nc, mu=mu, torque_rows=True, tau_max=float(np.quantile(np.abs(tf[:, 6:]), 0.4)))
+    _, x_r, st_r, _, rep = oracle_lib.contact_batch(prob, inp)
+    cases = np.where((st_r == 0) & (rep != 0))[0][:12]
+    assert len(cases) >= 8
+    faces_held = 0
+    for b in cases:
+        A, bb, lo, hi, groups, wth = ref.zspace(prob, inp, b)
+        z, st, fm, it, capped, pins = ref.lsi_level0(A, bb, lo, hi, groups, mu)
+        assert not capped
+        faces_held += sum(bin(m).count("1") for m in fm.values())
+        assert kkt.lsi_certificate(A, bb, z, lo, hi, groups, mu) <= TOL
+        zp = z.copy()
+        zp[groups[0] + 2] *= 1.0 + 1e-4  # one contact's normal force off its optimum
+        assert kkt.lsi_certificate(A, bb, zp, lo, hi, groups, mu) > TOL
+        y = A @ z - wth
+        yr = inp["Jw"][b] @ x_r[b, :n]
+        assert np.abs(y - yr).max() <= 1e-6 * max(1.0, np.abs(yr).max()), (b, np.abs(y - yr).max())
+    assert faces_held > 0  # the pyramid really binds in this sweep
