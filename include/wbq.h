@@ -112,6 +112,14 @@ typedef struct {
     int joint_limits;
     const double *q_min, *q_max; /* [n] joint position limits (ModelInterface::getJointLimits) */
     const double *Kjl, *Djl;     /* [n] barrier stiffness / damping */
+    /* Priority level of each Cartesian task: 0 the first level (its tasks summed), 1 a middle level
+     * between it and the joint task -- the elbow level the reference builds and leaves commented out
+     * of its stack (QPPVMPlugin.cpp:154-166 _elbow_task_left/right, :177-178):
+     *   ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits  = task_level {0, 0, 1, 1}.
+     * The middle level is lexicographic: min ||A1 x - b1||^2 keeping level 0 at its optimum y0*, and
+     * the joint task then keeps both. All zero (a zero-initialised tail): the reference stack.
+     * Needs W1 = I and n <= 32 (else wbq_create returns WBQ_E_UNSUPPORTED). */
+    int task_level[4];
 } wbq_desc;
 
 typedef struct {
@@ -205,6 +213,17 @@ int wbq_set_timing(wbq_ctx *ctx, int enable);
 int wbq_get_timing(wbq_ctx *ctx, double *total_ms, int *launches);
 /* Same, split: summed device time of whole solves and of their dominant (first) kernel. */
 int wbq_get_timing_detail(wbq_ctx *ctx, double *solve_ms, double *kernel_ms, int *launches);
+/* Per-context execution options (path choices that never change a result; the tests run both ways):
+ *   WBQ_OPT_INLINE_REPAIR   QPPVM W1 = I, n <= 32: -1 (default) the level-0 repair runs inside the
+ *                           fast kernel for 64 solves after a solve that needed it, else in its own
+ *                           follow-up kernel; 0 always the follow-up kernel; 1 always inline
+ *   WBQ_OPT_FUSED_ROLLOUT   1 (default) wbq_rollout of a QPPVM W1 = I context with n <= 32 runs all
+ *                           steps in one launch; 0 one launch per step
+ * The environment variables WBQ_INLREP / WBQ_FUSED_ROLLOUT, when set, give the initial values of a
+ * new context. */
+#define WBQ_OPT_INLINE_REPAIR 1
+#define WBQ_OPT_FUSED_ROLLOUT 2
+int wbq_set_option(wbq_ctx *ctx, int option, int value);
 void wbq_destroy(wbq_ctx *ctx);
 const char *wbq_last_error(const wbq_ctx *ctx);
 const char *wbq_version(void);

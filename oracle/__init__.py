@@ -34,7 +34,7 @@ class _Desc(ctypes.Structure):
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
                 ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
                 ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
-                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p)]
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4)]
 
 
 class _Inst(ctypes.Structure):
@@ -56,6 +56,8 @@ def lib():
         _lib.wbq_ref_level0.restype = ctypes.c_int
         _lib.wbq_ref_level1.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, P, P, P, P, P, P]
         _lib.wbq_ref_level1.restype = ctypes.c_int
+        _lib.wbq_ref_level_mid.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, P]
+        _lib.wbq_ref_level_mid.restype = ctypes.c_int
         _lib.wbq_ref_qppvm_one.argtypes = [P, P, P, P, P]
         _lib.wbq_ref_qppvm_one.restype = ctypes.c_int
         _lib.wbq_ref_qppvm_batch.argtypes = [P, ctypes.c_int] + [P] * 8 + [P, P, P]
@@ -86,6 +88,8 @@ def _desc(prob):
     for t in range(4):
         d.row_mask[t] = prob.row_mask[t] if t < prob.ntasks else 0
     d.select_mode, d.joint_weight = prob.select_mode, prob.joint_weight
+    for t, lv in enumerate(getattr(prob, "task_level", None) or ()):
+        d.task_level[t] = int(lv)
     keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
             for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
     d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [a.ctypes.data for a in keep]
@@ -114,6 +118,8 @@ def _inst(inputs, b):
 
 
 def assemble(prob, inputs, b=0):
+    """A0 [m0][n] / b0: the Cartesian rows, level-0 rows first, then the middle level's (prob.m_l0
+    of them are level 0)."""
     n = prob.n
     d, keep = _desc(prob)
     s, arrs = _inst(inputs, b)

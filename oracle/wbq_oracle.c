@@ -164,8 +164,18 @@ static void jacobi_svd(int R, int C, double *X, double *V, double *sig)
 
 /* Minimum-norm least squares over the columns F of A (m x n): z = pinv(A_F) r, via the SVD
  * of A_F^T (k x m): A_F^T V = U S  =>  A_F = V S U^T  =>  pinv(A_F) = U S^-1 V^T. */
+static void minnorm_ls_floor(int m, int n, const double *A, const int *F, int k, const double *r, double *z,
+                             double floor);
 static void minnorm_ls(int m, int n, const double *A, const int *F, int k, const double *r,
                        double *z)
+{
+    minnorm_ls_floor(m, n, A, F, k, r, z, 0.0);
+}
+
+/* Same, singular values also dropped below an absolute floor (a matrix that is zero up to roundoff
+ * has no directions: a relative cut would keep its roundoff). */
+static void minnorm_ls_floor(int m, int n, const double *A, const int *F, int k, const double *r, double *z,
+                             double floor)
 {
     double *X = (double *)malloc(sizeof(double) * (k > 0 ? k : 1) * m);
     double *V = (double *)malloc(sizeof(double) * m * m);
@@ -180,7 +190,7 @@ static void minnorm_ls(int m, int n, const double *A, const int *F, int k, const
         double s = 0.0;
         for (int a = 0; a < m; ++a) s += V[a * m + j] * r[a];
         /* U_j = X_j / sig_j, and z = sum_j U_j (V_j . r) / sig_j  => X_j (V_j . r) / sig_j^2 */
-        t[j] = (sig[j] > 1e-13 * smax) ? s / (sig[j] * sig[j]) : 0.0;
+        t[j] = (sig[j] > 1e-13 * smax && sig[j] > floor) ? s / (sig[j] * sig[j]) : 0.0;
     }
     for (int c = 0; c < k; ++c) {
         double s = 0.0;
@@ -260,8 +270,11 @@ int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *
         m0 = -WBQ_REF_NUMERICAL;
         goto done;
     }
-    /* ---- level 0: Cartesian impedance tasks (QPPVMPlugin.cpp:129-152), summed (:177) */
-    for (int t = 0; t < d->ntasks; ++t) {
+    /* ---- level 0: Cartesian impedance tasks (QPPVMPlugin.cpp:129-152), summed (:177); with a middle
+     * level (task_level, the elbow tasks :154-166,178) its tasks' rows follow the level-0 rows */
+    for (int tt = 0; tt < 2 * d->ntasks; ++tt) {
+        const int t = tt % d->ntasks;
+        if ((d->task_level[t] != 0) != (tt >= d->ntasks)) continue;
         const double *J = in->J + (size_t)t * 6 * n;
         double e[6], xdot[6], F[6], b6[6];
         wbq_ref_cart_error(in->pose + 12 * t, in->pose_ref + 12 * t, e);
@@ -493,6 +506,226 @@ out:
     return status;
 }
 
+int wbq_ref_task_rows(const wbq_ref_desc *d, int *m_l0)
+{
+    int m = 0, m0 = 0;
+    for (int t = 0; t < d->ntasks; ++t)
+        for (int r = 0; r < 6; ++r)
+            if ((d->row_mask[t] >> r) & 1) {
+                ++m;
+                if (d->task_level[t] == 0) ++m0;
+            }
+    if (m_l0) *m_l0 = m0;
+    return m;
+}
+
+/* ----------------------------------------------------------- middle level */
+
+/* Free-set step of the middle level: d = argmin ||A_F d - r|| over d in null(E_F), minimum norm.
+ * With E_F^T = U S V^T (one-sided Jacobi), P = I - U U^T projects onto null(E_F) and the minimum-norm
+ * solution of (A_F P) t = r lies in range(P A_F^T), so d = t already meets E_F d = 0. Returns 0 when
+ * null(E_F) is empty (d = 0): then P is zero up to roundoff, which the solve must not amplify. */
+static int mid_step(int me, const double *E, int m, int n, const double *A, const int *F, int k, const double *r,
+                    double *d)
+{
+    const int mq = me > 0 ? me : 1, kq = k > 0 ? k : 1;
+    double *X = (double *)malloc(sizeof(double) * kq * mq);
+    double *V = (double *)malloc(sizeof(double) * mq * mq);
+    double *sig = (double *)malloc(sizeof(double) * mq);
+    double *P = (double *)malloc(sizeof(double) * kq * kq);
+    double *B = (double *)malloc(sizeof(double) * m * kq);
+    int *all = (int *)malloc(sizeof(int) * kq);
+    for (int c = 0; c < k; ++c)
+        for (int a = 0; a < me; ++a) X[c * me + a] = E[a * n + F[c]];
+    for (int i = 0; i < k * k; ++i) P[i] = (i % (k + 1) == 0) ? 1.0 : 0.0;
+    int rank = 0;
+    if (me > 0 && k > 0) {
+        jacobi_svd(k, me, X, V, sig);
+        double smax = 0.0;
+        for (int j = 0; j < me; ++j) smax = dmax(smax, sig[j]);
+        for (int j = 0; j < me; ++j) {
+            if (!(sig[j] > 1e-12 * smax)) continue;
+            ++rank;
+            for (int a = 0; a < k; ++a)
+                for (int c = 0; c < k; ++c) P[a * k + c] -= X[a * me + j] * X[c * me + j] / (sig[j] * sig[j]);
+        }
+    }
+    double amax = 0.0;
+    for (int a = 0; a < m; ++a)
+        for (int c = 0; c < k; ++c) amax = dmax(amax, fabs(A[a * n + F[c]]));
+    if (rank >= k || k == 0) {
+        for (int c = 0; c < k; ++c) d[c] = 0.0;
+        free(X);
+        free(V);
+        free(sig);
+        free(P);
+        free(B);
+        free(all);
+        return 0;
+    }
+    for (int a = 0; a < m; ++a)
+        for (int c = 0; c < k; ++c) {
+            double s = 0.0;
+            for (int q = 0; q < k; ++q) s += A[a * n + F[q]] * P[q * k + c];
+            B[a * k + c] = s;
+        }
+    for (int c = 0; c < k; ++c) all[c] = c;
+    minnorm_ls_floor(m, k, B, all, k, r, d, 1e-12 * amax * sqrt((double)k));
+    free(X);
+    free(V);
+    free(sig);
+    free(P);
+    free(B);
+    free(all);
+    return 1;
+}
+
+/* multipliers of the bound variables at x: w = A^T (b - A x) - E^T nu, nu the least-squares fit of the
+ * free variables' gradient by the equality rows (E_F^T nu = A_F^T (b - A x)) */
+static void mid_multipliers(int me, const double *E, int m, int n, const double *A, const double *b,
+                            const double *x, const int *F, int k, double *w)
+{
+    const int mq = me > 0 ? me : 1, kq = k > 0 ? k : 1;
+    double *r = (double *)malloc(sizeof(double) * m);
+    double *Et = (double *)malloc(sizeof(double) * kq * mq);
+    double *gF = (double *)malloc(sizeof(double) * kq);
+    double *nu = (double *)calloc((size_t)mq, sizeof(double));
+    int *all = (int *)malloc(sizeof(int) * mq);
+    for (int a = 0; a < m; ++a) {
+        double s = b[a];
+        for (int j = 0; j < n; ++j) s -= A[a * n + j] * x[j];
+        r[a] = s;
+    }
+    for (int j = 0; j < n; ++j) {
+        double s = 0.0;
+        for (int a = 0; a < m; ++a) s += A[a * n + j] * r[a];
+        w[j] = s;
+    }
+    if (me > 0 && k > 0) {
+        for (int c = 0; c < k; ++c) {
+            gF[c] = w[F[c]];
+            for (int a = 0; a < me; ++a) Et[c * me + a] = E[a * n + F[c]];
+        }
+        for (int a = 0; a < me; ++a) all[a] = a;
+        minnorm_ls(k, me, Et, all, me, gF, nu);
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int a = 0; a < me; ++a) s += E[a * n + j] * nu[a];
+            w[j] -= s;
+        }
+    }
+    free(r);
+    free(Et);
+    free(gF);
+    free(nu);
+    free(all);
+}
+
+int wbq_ref_level_mid(int me, const double *E, int m, int n, const double *A, const double *b, const double *lb,
+                      const double *ub, double *x, int *state, double *w_out, int *iters)
+{
+    int *F = (int *)malloc(sizeof(int) * n);
+    int *excl = (int *)calloc((size_t)n, sizeof(int));
+    double *r = (double *)malloc(sizeof(double) * m);
+    double *dz = (double *)malloc(sizeof(double) * n);
+    double *w = (double *)malloc(sizeof(double) * n);
+    int status = WBQ_REF_MAXITER, it = 0;
+    const int maxit = 50 * n + 100;
+    for (int i = 0; i < n; ++i) {
+        if (lb[i] == ub[i]) state[i] = -1;
+        if (state[i] < 0) x[i] = lb[i];
+        if (state[i] > 0) x[i] = ub[i];
+    }
+    double Abmax = 0.0, xmax = 1.0;
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int a = 0; a < m; ++a) s += A[a * n + i] * b[a];
+        Abmax = dmax(Abmax, fabs(s));
+        xmax = dmax(xmax, fabs(x[i]));
+    }
+    const double wtol = 1e-11 * dmax(1.0, Abmax);
+    int freed = -1;
+    while (it < maxit) {
+        for (;;) { /* inner loop: step on the free set inside null(E_F), interpolate back into the box */
+            ++it;
+            int k = 0;
+            for (int i = 0; i < n; ++i)
+                if (state[i] == 0) F[k++] = i;
+            if (k == 0) break;
+            for (int a = 0; a < m; ++a) {
+                double s = b[a];
+                for (int i = 0; i < n; ++i) s -= A[a * n + i] * x[i];
+                r[a] = s;
+            }
+            if (!mid_step(me, E, m, n, A, F, k, r, dz)) break; /* no direction left on the free set */
+            double dmx = 0.0;
+            for (int c = 0; c < k; ++c) dmx = dmax(dmx, fabs(dz[c]));
+            if (dmx <= 1e-15 * xmax) break; /* stationary on the free set */
+            double alpha = 1.0;
+            int jblk = -1;
+            for (int c = 0; c < k; ++c) {
+                const int i = F[c];
+                if (dz[c] < 0.0 && x[i] + dz[c] < lb[i]) {
+                    const double a = (lb[i] - x[i]) / dz[c];
+                    if (a < alpha) alpha = a, jblk = c;
+                } else if (dz[c] > 0.0 && x[i] + dz[c] > ub[i]) {
+                    const double a = (ub[i] - x[i]) / dz[c];
+                    if (a < alpha) alpha = a, jblk = c;
+                }
+            }
+            if (jblk < 0) {
+                for (int c = 0; c < k; ++c) x[F[c]] += dz[c];
+                freed = -1;
+                for (int i = 0; i < n; ++i) excl[i] = 0;
+                break;
+            }
+            if (alpha < 0.0) alpha = 0.0;
+            if (F[jblk] == freed && alpha == 0.0) { /* Stark-Parker: re-bind, exclude */
+                const int i = F[jblk];
+                excl[i] = 1;
+                state[i] = dz[jblk] < 0.0 ? -1 : 1;
+                x[i] = state[i] < 0 ? lb[i] : ub[i];
+                freed = -1;
+                break;
+            }
+            for (int i = 0; i < n; ++i) excl[i] = 0;
+            for (int c = 0; c < k; ++c) x[F[c]] += alpha * dz[c];
+            {
+                const int i = F[jblk];
+                state[i] = dz[jblk] < 0.0 ? -1 : 1;
+                x[i] = state[i] < 0 ? lb[i] : ub[i];
+            }
+            freed = -1;
+            if (it >= maxit) break;
+        }
+        int k = 0;
+        for (int i = 0; i < n; ++i)
+            if (state[i] == 0) F[k++] = i;
+        mid_multipliers(me, E, m, n, A, b, x, F, k, w);
+        int best = -1;
+        double bestv = wtol;
+        for (int i = 0; i < n; ++i) {
+            if (state[i] == 0 || excl[i] || lb[i] == ub[i]) continue;
+            const double v = (state[i] < 0) ? w[i] : -w[i];
+            if (v > bestv) bestv = v, best = i;
+        }
+        if (best < 0) {
+            status = WBQ_REF_OK;
+            break;
+        }
+        state[best] = 0;
+        freed = best;
+    }
+    if (w_out) memcpy(w_out, w, sizeof(double) * n);
+    if (iters) *iters = it;
+    free(F);
+    free(excl);
+    free(r);
+    free(dz);
+    free(w);
+    return status;
+}
+
 /* ---------------------------------------------------------------- level 1 */
 
 int wbq_ref_level1(int n, const double *H, const double *g, int me, const double *Aeq,
@@ -649,9 +882,8 @@ int wbq_ref_qppvm_one(const wbq_ref_desc *d, const wbq_ref_instance *in, double 
                       int *iters)
 {
     const int n = d->n;
-    int m0max = 0;
-    for (int t = 0; t < d->ntasks; ++t)
-        for (int r = 0; r < 6; ++r) m0max += (d->row_mask[t] >> r) & 1;
+    int m_l0 = 0;
+    const int m0max = wbq_ref_task_rows(d, &m_l0);
     double *A0 = (double *)malloc(sizeof(double) * (m0max + 1) * n);
     double *b0 = (double *)malloc(sizeof(double) * (m0max + 1));
     double *y = (double *)malloc(sizeof(double) * (m0max + 1));
@@ -668,32 +900,63 @@ int wbq_ref_qppvm_one(const wbq_ref_desc *d, const wbq_ref_instance *in, double 
         status = -m0;
         goto fallback;
     }
-    status = wbq_ref_level0(m0, n, A0, b0, lb, ub, x, state, &it0);
-    if (status != WBQ_REF_OK) goto fallback;
-    for (int a = 0; a < m0; ++a) {
-        double s = 0.0;
-        for (int j = 0; j < n; ++j) s += A0[a * n + j] * x[j];
-        y[a] = s;
-    }
-    if (y0) memcpy(y0, y, sizeof(double) * m0);
     {
+        /* level 0 over its own rows (the first m_l0; all of them in the reference stack) */
+        const int ml = m0 - (m0max - m_l0);
+        status = wbq_ref_level0(ml, n, A0, b0, lb, ub, x, state, &it0);
+        if (status != WBQ_REF_OK) goto fallback;
+        for (int a = 0; a < ml; ++a) {
+            double s = 0.0;
+            for (int j = 0; j < n; ++j) s += A0[a * n + j] * x[j];
+            y[a] = s;
+        }
         /* Variables the level-0 gradient w = A0^T (b0 - y*) pins to a bound sit at that bound
          * in every level-0 optimum, hence everywhere in level 1's feasible set: fix them. */
         double wmax = 1.0;
         for (int j = 0; j < n; ++j) {
             double s = 0.0;
-            for (int a = 0; a < m0; ++a) s += A0[a * n + j] * b0[a];
+            for (int a = 0; a < ml; ++a) s += A0[a * n + j] * b0[a];
             wmax = dmax(wmax, fabs(s));
         }
         for (int j = 0; j < n; ++j) {
             double w = 0.0;
-            for (int a = 0; a < m0; ++a) w += A0[a * n + j] * (b0[a] - y[a]);
+            for (int a = 0; a < ml; ++a) w += A0[a * n + j] * (b0[a] - y[a]);
             if (w > 1e-9 * wmax) lb[j] = ub[j];
             else if (w < -1e-9 * wmax) ub[j] = lb[j];
             if (x[j] < lb[j]) x[j] = lb[j];
             if (x[j] > ub[j]) x[j] = ub[j];
         }
+        if (ml < m0) {
+            /* the middle level (the elbow tasks): its optimum y1* keeping level 0 at y0*, then the
+             * variables its multipliers hold at a bound are fixed too */
+            const int m1 = m0 - ml;
+            double *w = (double *)malloc(sizeof(double) * n);
+            int itm = 0;
+            status = wbq_ref_level_mid(ml, A0, m1, n, A0 + (size_t)ml * n, b0 + ml, lb, ub, x, state, w, &itm);
+            it0 += itm;
+            if (status == WBQ_REF_OK) {
+                for (int a = ml; a < m0; ++a) {
+                    double s = 0.0;
+                    for (int j = 0; j < n; ++j) s += A0[a * n + j] * x[j];
+                    y[a] = s;
+                }
+                double wm = 1.0;
+                for (int j = 0; j < n; ++j) {
+                    double s = 0.0;
+                    for (int a = ml; a < m0; ++a) s += A0[a * n + j] * b0[a];
+                    wm = dmax(wm, fabs(s));
+                }
+                for (int j = 0; j < n; ++j) {
+                    if (lb[j] == ub[j] || state[j] == 0) continue;
+                    if (state[j] < 0 && w[j] < -1e-9 * wm) ub[j] = lb[j];
+                    if (state[j] > 0 && w[j] > 1e-9 * wm) lb[j] = ub[j];
+                }
+            }
+            free(w);
+            if (status != WBQ_REF_OK) goto fallback;
+        }
     }
+    if (y0) memcpy(y0, y, sizeof(double) * m0);
     status = wbq_ref_level1(n, H1, g1, m0, A0, y, lb, ub, x, state, &it1);
     if (status != WBQ_REF_OK) goto fallback;
     for (int j = 0; j < n; ++j) tau[j] = x[j] + in->h[j];

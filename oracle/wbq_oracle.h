@@ -73,6 +73,11 @@ typedef struct {
      * Kjl (q_min - q) - Djl qd <= tau <= Kjl (q_max - q) - Djl qd */
     int joint_limits;
     const double *q_min, *q_max, *Kjl, *Djl; /* [n] */
+    /* priority level of each Cartesian task (include/wbq.h task_level): 0 the first level (the
+     * tasks there summed), 1 a middle level between it and the joint task -- the elbow level of
+     * QPPVMPlugin.cpp:154-166,177-178, ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits.
+     * All zero: the reference stack. */
+    int task_level[WBQ_REF_MAX_TASKS];
 } wbq_ref_desc;
 
 /* One instance (all row-major fp64):
@@ -99,6 +104,18 @@ int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *
  * Returns a WBQ_REF_* status. */
 int wbq_ref_level0(int m, int n, const double *A, const double *b, const double *lb,
                    const double *ub, double *x, int *state, int *iters);
+
+/* Rows of the stacked Cartesian tasks per level: returns the total m (level-0 rows first, then the
+ * middle level's, as wbq_ref_assemble orders them) and sets *m_l0 to the level-0 count. */
+int wbq_ref_task_rows(const wbq_ref_desc *d, int *m_l0);
+
+/* Middle level: min 0.5||A x - b||^2 s.t. E x = e (level-0 optimality, me rows), lb <= x <= ub,
+ * from a feasible x with bound state[n] (the level-0 solution): Stark-Parker BVLS whose free-set
+ * solves stay in the null space of E's free columns (minimum-norm, SVD); multipliers of the bound
+ * variables w = A^T (b - A x) - E^T nu. Returns a WBQ_REF_* status; w_out [n] (optional) the
+ * final w (pins). */
+int wbq_ref_level_mid(int me, const double *E, int m, int n, const double *A, const double *b, const double *lb,
+                      const double *ub, double *x, int *state, double *w_out, int *iters);
 
 /* Level 1: strictly convex QP min 0.5 x^T H x + g^T x s.t. Aeq x = beq, lb <= x <= ub,
  * primal active set (qpOASES family) started from a feasible x with bound state[n]. */

@@ -26,12 +26,16 @@ def _headers(src: str | None = None) -> list:
         with open(todo.pop()) as f:
             for line in f:
                 line = line.strip()
-                if line.startswith("#include \""):
-                    h = os.path.join(CSRC, line.split('"')[1])
-                    if os.path.exists(h) and h not in seen:
-                        seen.append(h)
-                        todo.append(h)
-    return sorted(seen) + inc
+                if line.startswith("#include \"") or line.startswith("#include <wbq"):
+                    name = line.split('"')[1] if '"' in line else line.split("<")[1].split(">")[0]
+                    for d in (CSRC, os.path.join(ROOT, "include")):
+                        h = os.path.join(d, name)
+                        if os.path.exists(h):
+                            if h not in seen:
+                                seen.append(h)
+                                todo.append(h)
+                            break
+    return sorted(seen)
 
 
 def _digest(flags: list, paths: list) -> str:
@@ -82,6 +86,8 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     objdir = os.path.join(HERE, "build", "obj")
     os.makedirs(objdir, exist_ok=True)
     hdrs = _headers()
+    # the record is taken before compiling: an edit made while the build runs leaves it stale
+    record = _digest(_FLAGS_KEY, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
     objs = [os.path.join(objdir, os.path.splitext(s)[0] + "_" +
                          _digest(flags, [os.path.join(CSRC, s)] + _headers(os.path.join(CSRC, s))) + ".o")
             for s in SOURCES]
@@ -103,7 +109,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     os.replace(lib + ".tmp", lib)
     if lib == LIB and not defines:
         with open(_stamp(LIB), "w") as f:
-            f.write(_digest(_FLAGS_KEY, [os.path.join(CSRC, s) for s in SOURCES] + hdrs) + "\n")
+            f.write(record + "\n")
     return lib
 
 

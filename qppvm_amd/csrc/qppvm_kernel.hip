@@ -571,8 +571,10 @@ constexpr int kNp64OneRound = 1024;
 // MR: rows of M loaded (n <= MR, compile time; the rest of the NP padding rows are identity
 // without a load): with n = 39 and MR = 40 the stage issues ~59 loads per lane instead of ~83,
 // under the 63 outstanding vector memory operations.
-template <int NP, int M0, bool MERGED, int TM, int W, int MR, bool INLREP = false>
-__global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
+// ROLL (qppvm_rollout_kernel): one step of a fused rollout -- no work-list bookkeeping (the repair is
+// inline, INLREP), the launch's counters are reset once by the caller.
+template <int NP, int M0, bool MERGED, int TM, int W, int MR, bool INLREP, bool ROLL>
+__device__ __forceinline__ void fast_body(const QppvmArgs &a)
 {
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -589,7 +591,8 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     const int ic = i < n ? i : n - 1; // clamped column for unconditional loads
     // INLREP (no follow-up kernel publishes counts): the previous solve's counts, complete by
     // stream order, for the host's choice of the next solve's variant (FollowGrid)
-    if constexpr (MERGED && INLREP) follow_publish(a.fg, a.work[(a.epoch ^ 1) * 2], a.work[(a.epoch ^ 1) * 2 + 1]);
+    if constexpr (MERGED && INLREP && !ROLL)
+        follow_publish(a.fg, a.work[(a.epoch ^ 1) * 2], a.work[(a.epoch ^ 1) * 2 + 1]);
     WBQ_RTSTAMP(16);
     WBQ_STAMP(0);
 
@@ -934,7 +937,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
     WBQ_STAMP(5);
     if constexpr (MERGED && INLREP) {
         // one launch per solve: no follow-up kernel resets the next solve's work counters
-        if (blockIdx.x == 0 && tid == 0) {
+        if (!ROLL && blockIdx.x == 0 && tid == 0) {
             a.work[(a.epoch ^ 1) * 2] = 0;
             a.work[(a.epoch ^ 1) * 2 + 1] = 0;
         }
@@ -942,12 +945,39 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
         // its register demand does not reach the fast path (inlined inside the active-set branch
         // it spilled there)
         if (__any(rep_inl)) {
-            if (rep_inl && i == 0) atomicAdd(a.work + a.epoch * 2 + 1, 1); // the repair count (grid policy)
+            if (!ROLL && rep_inl && i == 0) atomicAdd(a.work + a.epoch * 2 + 1, 1); // the repair count (grid policy)
             __syncthreads();
             repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
         }
     }
     WBQ_RTSTAMP(17);
+}
+
+template <int NP, int M0, bool MERGED, int TM, int W, int MR, bool INLREP = false>
+__global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
+{
+    fast_body<NP, M0, MERGED, TM, W, MR, INLREP, false>(a);
+}
+
+// MPC rollout in one launch (wbq_rollout): every wave runs its instances'
+// `steps` integrating solves back to back -- the fast path, the dual active set and the level-0 repair
+// inline -- carrying q, qd (rollout_step) and the warm-start state (ws_hint, ws_rows, ws_state) from
+// step to step through its own global rows. The same work as `steps` launches of the inline-repair
+// fast kernel; without the per-step launch boundary an instance whose repair runs long delays only its
+// own wave instead of every instance's next step (config 4 with per-step launches: the rare repaired
+// instance-steps, ~0.3 %, held whole launches for hundreds of microseconds).
+template <int NP, int M0, int TM>
+__global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // one launch: the next solve's counters (as INLREP)
+        a.work[(a.epoch ^ 1) * 2] = 0;
+        a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+    }
+#pragma unroll 1
+    for (int s = 0; s < a.steps; ++s) {
+        fast_body<NP, M0, true, TM, 2, 32, true, true>(a);
+        __syncthreads(); // this wave's q, qd and warm-start writes are visible to its next step
+    }
 }
 
 template <int NP, typename Lay, typename K>
@@ -972,6 +1002,16 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
     using Lay = FastLdsLayout<NP, MERGED>;
     hipError_t e;
+    if constexpr (NP == 32 && kInlineRepair<M0>) { // a whole rollout in one launch
+        if (a.steps > 0 || a.prepare) {
+            e = a.ntasks <= 2 ? launch_one<NP, Lay>(qppvm_rollout_kernel<NP, M0, 2>, a, grid, stream)
+                              : launch_one<NP, Lay>(qppvm_rollout_kernel<NP, M0, kTMax>, a, grid, stream);
+            if (e != hipSuccess || !a.prepare) {
+                if (e == hipSuccess && mid) e = hipEventRecord(mid, stream);
+                return e;
+            }
+        }
+    }
     if constexpr (NP == 32) {
         // (the inline repair only where it keeps 2 waves per SIMD: M0 <= 6)
         const bool inl = kInlineRepair<M0> && (a.inline_repair || a.prepare);

@@ -18,6 +18,12 @@
 #include "../../include/wbq.h"
 #include "wbq_kernels.h"
 
+static int env_option(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 struct wbq_ctx {
     int device = 0;
     int form = WBQ_FORM_QPPVM;
@@ -76,6 +82,9 @@ struct wbq_ctx {
     size_t np = 0;
     int epoch = 0;
     int inl_hold = 0; // solves left in the inline-repair variant since a solve last needed a repair
+    // per-context options (wbq_set_option); the environment gives a new context's initial values
+    int opt_inline = env_option("WBQ_INLREP", -1); // WBQ_OPT_INLINE_REPAIR
+    int opt_fused = env_option("WBQ_FUSED_ROLLOUT", 1); // WBQ_OPT_FUSED_ROLLOUT
     // follow-up grid sizing (wbq_kernels.h FollowGrid): counts the last follow-up kernel saw, in
     // mapped pinned host memory (device view work_seen_dev), and the host's running estimate
     int *work_seen = nullptr, *work_seen_dev = nullptr;
@@ -543,7 +552,8 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
 // prepare: raise the LDS limits of every kernel variant this context can launch, launch nothing
 // (wbq_create*: the solve path then takes no lock and does not allocate). rbd: re-evaluate the model
 // in place first (wbq_rollout_rbd), inside the timed window of a timed solve.
-static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false, const wbq_rbd_ctx *rbd = nullptr)
+static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false, const wbq_rbd_ctx *rbd = nullptr,
+                      int steps = 0)
 {
     if (!c) return WBQ_E_INVALID;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "wbq_set_inputs not called");
@@ -606,17 +616,17 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.integrate = integrate;
     a.dt = dt;
     a.prepare = prepare ? 1 : 0;
+    a.steps = steps;
     {
         // n <= 32: the level-0 repair runs inside the fast kernel when the last solves needed it
         // (one launch per solve instead of a follow-up launch that waits for the whole fast kernel:
         // config 4 7.8 -> 9.8 M QP/s), in qppvm_repair_kernel otherwise (the inline variant's fast
         // path is ~5 us slower than the ~3 us that launch costs: config 1). WBQ_INLREP=0/1 forces it.
-        static const int env_inl = [] { const char *e = getenv("WBQ_INLREP"); return e ? atoi(e) : -1; }();
         // (held for 64 solves after the last repair seen: rollouts repair a few instances now and then)
         const int seen1 = c->work_seen ? __atomic_load_n(c->work_seen + 1, __ATOMIC_RELAXED) : 0;
         if (seen1 > 0) c->inl_hold = 64;
         else if (c->inl_hold > 0) --c->inl_hold;
-        a.inline_repair = env_inl >= 0 ? env_inl : (c->inl_hold > 0 ? 1 : 0);
+        a.inline_repair = c->opt_inline >= 0 ? c->opt_inline : (c->inl_hold > 0 ? 1 : 0);
     }
 
     WBQ_HIP(hipSetDevice(c->device));
@@ -644,10 +654,32 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
 
 int wbq_solve(wbq_ctx *c) { return solve_impl(c, 0, 0.0); }
 
+int wbq_set_option(wbq_ctx *c, int option, int value)
+{
+    if (!c) return WBQ_E_INVALID;
+    switch (option) {
+    case WBQ_OPT_INLINE_REPAIR:
+        if (value < -1 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_INLINE_REPAIR: -1, 0 or 1");
+        c->opt_inline = value;
+        return WBQ_SUCCESS;
+    case WBQ_OPT_FUSED_ROLLOUT:
+        if (value < 0 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_FUSED_ROLLOUT: 0 or 1");
+        c->opt_fused = value;
+        return WBQ_SUCCESS;
+    default:
+        return fail(c, WBQ_E_INVALID, "wbq_set_option: unknown option");
+    }
+}
+
 int wbq_rollout(wbq_ctx *c, int steps, double dt)
 {
     if (!c) return WBQ_E_INVALID;
     if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout: steps >= 0, dt >= 0");
+    // QPPVM W1 = I with n <= 32 and m0 <= 6: the whole rollout in one launch (qppvm_rollout_kernel);
+    // WBQ_OPT_FUSED_ROLLOUT = 0 keeps one launch per step (the A/B of the two)
+    if (c->opt_fused && steps > 0 && c->form == WBQ_FORM_QPPVM && c->d.joint_weight == WBQ_WEIGHT_IDENTITY &&
+        c->d.n <= 32 && c->m0 <= 6)
+        return solve_impl(c, 1, dt, false, nullptr, steps);
     for (int k = 0; k < steps; ++k) {
         const int rc = solve_impl(c, 1, dt);
         if (rc != WBQ_SUCCESS) return rc;

@@ -99,6 +99,10 @@ struct QppvmArgs {
     // NP = 32: the level-0 repair runs at the end of the fast kernel (one launch per solve) instead
     // of in qppvm_repair_kernel
     int inline_repair;
+    // > 0: the whole rollout of `steps` integrating solves in one launch (qppvm_rollout_kernel, NP =
+    // 32, M0 <= 6): every wave carries its instances through all steps, so an instance that needs a
+    // long level-0 repair in some step holds only its own wave, not every instance's next step
+    int steps;
 };
 
 // The box on x = tau - h of joint j (QPPVMPlugin.cpp:203-205: tau limits shifted by -h; with the

@@ -72,6 +72,10 @@ class QPPVMProblem:
     q_max: np.ndarray | float = np.pi
     Kjl: np.ndarray | float = 50.0
     Djl: np.ndarray | float = 20.0
+    # priority level per Cartesian task: 0 = the first level (summed), 1 = a middle level between it
+    # and the joint task -- the elbow level QPPVMPlugin.cpp:154-166,177-178 leaves commented out,
+    # ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits (include/wbq.h task_level). None: all 0.
+    task_level: tuple | None = None
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -87,6 +91,10 @@ class QPPVMProblem:
         if len(rm) != T or any(not (0 < m < 64) for m in rm):
             raise ValueError("row_mask needs one non-empty 6-bit mask per task")
         self.row_mask = rm
+        tl = (0,) * T if self.task_level is None else tuple(int(v) for v in self.task_level)
+        if len(tl) != T or any(v not in (0, 1) for v in tl) or 0 not in tl:
+            raise ValueError("task_level needs one level (0 or 1) per task, at least one task on level 0")
+        self.task_level = tl
         kc = np.asarray(self.Kc, dtype=np.float64)
         dc = np.asarray(self.Dc, dtype=np.float64)
         self.Kc = np.ascontiguousarray(np.broadcast_to(kc, (T, 6)).astype(np.float64))
@@ -105,8 +113,13 @@ class QPPVMProblem:
 
     @property
     def m0(self) -> int:
-        """Rows of level 0 (sum of selected task rows)."""
+        """Rows of the Cartesian levels (sum of selected task rows, the middle level included)."""
         return sum(bin(m).count("1") for m in self.row_mask)
+
+    @property
+    def m_l0(self) -> int:
+        """Rows of the first level alone (m0 in the reference stack)."""
+        return sum(bin(m).count("1") for m, lv in zip(self.row_mask, self.task_level) if lv == 0)
 
 
 # per-instance input arrays and their shapes (B = batch)

@@ -27,7 +27,7 @@ EXPORTS = ("wbq_create", "wbq_set_stream", "wbq_set_inputs", "wbq_solve", "wbq_s
            "wbq_get_timing", "wbq_destroy", "wbq_last_error", "wbq_version", "wbq_create_contact",
            "wbq_set_contact_inputs", "wbq_get_contact_outputs", "wbq_get_timing_detail", "wbq_rollout",
            "wbq_get_state", "wbq_set_state", "wbq_get_warmstart_hints", "wbq_rbd_create", "wbq_rbd_compute",
-           "wbq_rbd_set_stream", "wbq_rbd_destroy", "wbq_rollout_rbd", "wbq_rbd_compute_ex")
+           "wbq_rbd_set_stream", "wbq_rbd_destroy", "wbq_rollout_rbd", "wbq_rbd_compute_ex", "wbq_set_option")
 
 
 class WbqError(RuntimeError):
@@ -42,7 +42,7 @@ class Desc(ctypes.Structure):
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
                 ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
                 ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
-                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p)]
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4)]
 
 
 class Inputs(ctypes.Structure):
@@ -121,6 +121,7 @@ def load_library(path: str = LIB_PATH):
     lib.wbq_set_contact_inputs.argtypes = [P, ctypes.POINTER(ContactInputs)]
     lib.wbq_get_contact_outputs.argtypes = [P, P]
     lib.wbq_rollout.argtypes = [P, I, ctypes.c_double]
+    lib.wbq_set_option.argtypes = [P, I, I]
     lib.wbq_get_state.argtypes = [P, P, P]
     lib.wbq_set_state.argtypes = [P, P, P, I]
     lib.wbq_get_warmstart_hints.argtypes = [P, P]
@@ -161,6 +162,8 @@ class QPPVMSolver:
         for t in range(4):
             d.row_mask[t] = prob.row_mask[t] if t < prob.ntasks else 0
         d.select_mode, d.joint_weight = prob.select_mode, prob.joint_weight
+        for t, lv in enumerate(prob.task_level):
+            d.task_level[t] = int(lv)
         d.max_batch, d.max_iter = self.max_batch, int(prob.max_iter)
         self._keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
                       for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
@@ -240,6 +243,13 @@ class QPPVMSolver:
         self._check(self.lib.wbq_get_device_outputs(self.ctx, ctypes.byref(t), ctypes.byref(s),
                                                     ctypes.byref(i)), "wbq_get_device_outputs")
         return t.value, s.value, i.value
+
+    OPT_INLINE_REPAIR = 1  # include/wbq.h WBQ_OPT_*
+    OPT_FUSED_ROLLOUT = 2
+
+    def set_option(self, option: int, value: int):
+        """Per-context execution option (wbq_set_option): a path choice, never a result change."""
+        self._check(self.lib.wbq_set_option(self.ctx, int(option), int(value)), "wbq_set_option")
 
     def rollout(self, steps: int, dt: float = 1e-3):
         """``steps`` solves with q, qd integrated on the device between them (wbq_rollout)."""

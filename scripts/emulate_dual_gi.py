@@ -33,20 +33,27 @@ class Problem:
         self.n, self.nc, self.nx = n, nc, n + 3 * nc
         tr = bool(prob.torque_rows)
         NJ = n if tr else 6
-        self.NJ, self.ME = NJ, NJ + 6 + 3 * nc
+        mu = float(getattr(prob, "mu", 0.0))
+        nfr = 4 * nc if mu > 0 else 0
+        self.mu, self.nfr = mu, nfr
+        self.NJ, self.ME = NJ, NJ + 6 + 3 * nc + nfr
         cm = int(inp["cmask"][b])
         rows, lo, hi, kind = [], [], [], []
         for ci in range(NJ):
             if ci < 6:
                 rows.append(a["E"][6 + ci]); lo.append(a["e"][6 + ci]); hi.append(a["e"][6 + ci]); kind.append(1)
             else:
-                r = 3 * nc + ci - 6
+                r = 3 * nc + nfr + ci - 6
                 rows.append(a["C"][r]); lo.append(a["clo"][r]); hi.append(a["chi"][r]); kind.append(2)
         for r in range(6):
             rows.append(a["E"][r]); lo.append(a["e"][r]); hi.append(a["e"][r]); kind.append(1)
         for f in range(3 * nc):
             on = (cm >> (f // 3)) & 1
             rows.append(a["C"][f]); lo.append(a["clo"][f] if on else -INF); hi.append(a["chi"][f] if on else INF)
+            kind.append(2 if on else 0)
+        for f in range(nfr):  # friction faces (one-sided), after the force rows as in the kernel
+            on = (cm >> (f // 4)) & 1
+            rows.append(a["C"][3 * nc + f]); lo.append(-INF); hi.append(0.0 if on else INF)
             kind.append(2 if on else 0)
         self.A = np.array(rows)
         for c in range(nc):  # inactive contacts: their forces appear in no row (the kernel zeroes them)
@@ -125,6 +132,7 @@ def solve(P, maxit=None, delta=0.0, kdep=1e-14, trace=False, rounds_max=8, wkeep
     if sing:
         return 3, None, iters
     need_select, dirty, force_rebuild = True, True, False
+    just_dropped = False
     cp, sgp, bnd, lamp, peq = 0, 1.0, 0.0, 0.0, False
     x = None
     while True:
@@ -132,7 +140,8 @@ def solve(P, maxit=None, delta=0.0, kdep=1e-14, trace=False, rounds_max=8, wkeep
             v = np.full(m, -1.0)
             for j in range(m):
                 if kind[j] == 2 and not onact[j]:
-                    tol = 1e-10 * max(1.0, abs(s[j]), abs(lo[j]), abs(hi[j]))
+                    fin = lambda v: abs(v) if abs(v) < 1e299 else 0.0  # noqa: E731 (one-sided rows)
+                    tol = 1e-10 * max(1.0, abs(s[j]), fin(lo[j]), fin(hi[j]))
                     viol = max(lo[j] - s[j], s[j] - hi[j])
                     if viol > tol:
                         v[j] = viol / nrm[j]
@@ -219,7 +228,12 @@ def solve(P, maxit=None, delta=0.0, kdep=1e-14, trace=False, rounds_max=8, wkeep
         blk = int(np.argmin(cand)) if k else 0
         t1 = cand[blk] if k else INF
         dim = P.dim + (6 if delta > 0 else 0)  # the waist slacks add 6 primal dimensions
-        t2 = -slack / zz if (k < dim and zz > kdep * gpp) else INF
+        # AFTERDROP: p was dependent on the slots before the drop with a positive coefficient on the
+        # dropped one, so it is independent of the rest in exact arithmetic -- take its step when the
+        # computed complement is at least positive (EXPERIMENT)
+        after_drop = os.environ.get("AFTERDROP", "0") == "1" and just_dropped
+        t2 = -slack / zz if (k < dim and (zz > kdep * gpp or (after_drop and zz > 0))) else INF
+        just_dropped = False
         if trace:
             print(f"  it {iters}: cp={cp} sg={sgp:+.0f} k={k} slack={slack:.3e} zz={zz:.3e} d2={d2:.3e} "
                   f"gpp={gpp:.3e} t1={t1:.3e} (blk {blk}) t2={t2:.3e}")
@@ -249,6 +263,7 @@ def solve(P, maxit=None, delta=0.0, kdep=1e-14, trace=False, rounds_max=8, wkeep
             k += 1
             need_select = True
         else:
+            just_dropped = True
             onact[act[blk]] = False
             act[blk:k - 1], sgn[blk:k - 1], lam[blk:k - 1], aeq[blk:k - 1] = \
                 act[blk + 1:k].copy(), sgn[blk + 1:k].copy(), lam[blk + 1:k].copy(), aeq[blk + 1:k].copy()
@@ -287,29 +302,78 @@ def level0(P, prob, inp, b):
     bb = bw + W.T @ h
     zlo, zhi = np.array(zlo), np.array(zhi)
     fixed = zlo == zhi
-    A0f = A0[:, ~fixed]
-    r = lsq_linear(A0f, bb - A0[:, fixed] @ zlo[fixed], bounds=(zlo[~fixed], zhi[~fixed]), method="bvls",
-                   tol=1e-14, lsmr_tol=None)
-    z = zlo.copy()
-    z[~fixed] = r.x
-    ys = A0 @ z
-    g = A0.T @ (bb - ys)
-    abm = max(1.0, np.abs(A0.T @ bb).max())
     lo, hi = P.lo.copy(), P.hi.copy()
     NJ = P.NJ
-    for j in range(len(z)):
-        ci = 6 + j if j < n - 6 else NJ + 6 + (j - (n - 6))
-        if j < n - 6 and not prob.torque_rows:
-            continue
-        if g[j] > 1e-9 * abm:
-            lo[ci] = hi[ci]
-        elif g[j] < -1e-9 * abm:
-            hi[ci] = lo[ci]
-    lo[NJ:NJ + 6] = hi[NJ:NJ + 6] = ys - W.T @ h
-    # waist rows to keep: a pivot basis of the span of the unpinned columns (the others are
-    # implied by the pins)
-    unp = [j for j in range(len(z)) if not (abs(g[j]) > 1e-9 * abm) and not fixed[j]]
-    Gu = A0[:, unp] @ A0[:, unp].T if unp else np.zeros((6, 6))
+    abm = max(1.0, np.abs(A0.T @ bb).max())
+    if P.mu > 0:  # box + friction pyramid: the LSI of qppvm_amd/csrc/fric_lsi.h (tests/fric_lsi_ref.py)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import fric_lsi_ref as fr
+        groups = [n - 6 + 3 * c for c in range(nc) if (P.cm >> c) & 1]
+        z, st, fm, it, capped, pins = fr.lsi_level0(A0, bb, zlo, zhi, groups, P.mu)
+        ys = A0 @ z
+        ingroup = set(j for g0 in groups for j in range(g0, g0 + 3))
+        held = {}
+        for key, v in pins.items():
+            lamv = v if (key[0] == "face" or key[1] in ingroup) else -v
+            if lamv > 1e-9 * abm:
+                held[key] = True
+        pin = np.zeros(len(z), int)
+        for key in held:
+            if key[0] == "box":
+                pin[key[1]] = key[2]
+            else:
+                c = (key[1] - (n - 6)) // 3
+                lo[NJ + 6 + 3 * nc + 4 * c + key[2]] = 0.0
+        for j in range(len(z)):
+            ci = 6 + j if j < n - 6 else NJ + 6 + (j - (n - 6))
+            if j < n - 6 and not prob.torque_rows:
+                continue
+            if pin[j] > 0:
+                lo[ci] = hi[ci]
+            elif pin[j] < 0:
+                hi[ci] = lo[ci]
+        # movable columns: projector of each group onto the null space of its held constraints
+        cols_m = []
+        for j in range(len(z)):
+            if j in ingroup or fixed[j] or pin[j] != 0:
+                continue
+            cols_m.append(A0[:, j])
+        for g0 in groups:
+            N = []
+            for k in range(3):
+                if pin[g0 + k] != 0 or fixed[g0 + k]:
+                    e = np.zeros(3); e[k] = 1.0; N.append(e)
+            for key in held:
+                if key[0] == "face" and key[1] == g0:
+                    N.append(fr.face_normal(key[2], P.mu))
+            Pc = fr.projector(np.array(N).reshape(-1, 3))
+            for k in range(3):
+                cols_m.append(A0[:, g0:g0 + 3] @ Pc[:, k])
+        Am = np.array(cols_m).T if cols_m else np.zeros((6, 0))
+        Gu = Am @ Am.T
+        lo[NJ:NJ + 6] = hi[NJ:NJ + 6] = ys - W.T @ h
+        unp = [0]
+    else:
+        A0f = A0[:, ~fixed]
+        r = lsq_linear(A0f, bb - A0[:, fixed] @ zlo[fixed], bounds=(zlo[~fixed], zhi[~fixed]), method="bvls",
+                       tol=1e-14, lsmr_tol=None)
+        z = zlo.copy()
+        z[~fixed] = r.x
+        ys = A0 @ z
+        g = A0.T @ (bb - ys)
+        for j in range(len(z)):
+            ci = 6 + j if j < n - 6 else NJ + 6 + (j - (n - 6))
+            if j < n - 6 and not prob.torque_rows:
+                continue
+            if g[j] > 1e-9 * abm:
+                lo[ci] = hi[ci]
+            elif g[j] < -1e-9 * abm:
+                hi[ci] = lo[ci]
+        lo[NJ:NJ + 6] = hi[NJ:NJ + 6] = ys - W.T @ h
+        # waist rows to keep: a pivot basis of the span of the unpinned columns (the others are
+        # implied by the pins)
+        unp = [j for j in range(len(z)) if not (abs(g[j]) > 1e-9 * abm) and not fixed[j]]
+        Gu = A0[:, unp] @ A0[:, unp].T if unp else np.zeros((6, 6))
     keep, d = [], np.diag(Gu).copy()
     L = np.zeros((6, 6))
     dmx = max(d.max(), 1e-300)

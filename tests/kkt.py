@@ -28,7 +28,12 @@ def _active(v, lo, hi, tol):
 
 
 def qppvm_certificate(oracle, prob, inp, b, tau):
-    """Scaled residuals of instance b's output tau: dict(primal, level0, stat, sign, indep)."""
+    """Scaled residuals of instance b's output tau: dict(primal, level0, stat, sign, indep).
+    With a middle level (prob.task_level, the elbow tasks) the Cartesian rows form two lexicographic
+    levels: level 0 over the first prob.m_l0 rows as above, then the middle level
+    0.5 ||A1 x - b1||^2 over {A0 x = A0 x, box}: its gradient g1 = E^T nu + mu with E the level-0 rows,
+    nu fitted on the free variables, mu_j of the right sign at bounds the earlier level does not pin;
+    "level0" reports the worse of the two."""
     M = inp["M"][b]
     a = oracle.assemble(prob, inp, b)
     A0, b0, lb, ub = a["A0"], a["b0"], a["lb"], a["ub"]
@@ -37,13 +42,23 @@ def qppvm_certificate(oracle, prob, inp, b, tau):
     primal = max(0.0, (lb - x).max(), (x - ub).max()) / scale
     at_lo, at_hi = _active(x, lb, ub, 1e-9)
     free = ~(at_lo | at_hi)
-    g0 = A0.T @ (A0 @ x - b0)
-    s0 = np.abs(A0.T).sum(axis=1) * (np.abs(A0 @ x).max() + np.abs(b0).max()) + 1e-300
-    l0 = np.where(free, np.abs(g0), 0.0)
-    l0 = np.maximum(l0, np.where(at_lo & ~at_hi, np.maximum(-g0, 0.0), 0.0))
-    l0 = np.maximum(l0, np.where(at_hi & ~at_lo, np.maximum(g0, 0.0), 0.0))
-    level0 = float((l0 / s0).max())
-    pinned = np.abs(g0) > 1e-7 * s0  # level 0 holds these at their bound
+    ml = getattr(prob, "m_l0", A0.shape[0])
+    levels = [(A0[:ml], b0[:ml])] + ([(A0[ml:], b0[ml:])] if ml < A0.shape[0] else [])
+    pinned = lb == ub
+    level0, E = 0.0, None
+    for Al, bl in levels:
+        g0 = Al.T @ (Al @ x - bl)
+        s0 = np.abs(Al.T).sum(axis=1) * (np.abs(Al @ x).max() + np.abs(bl).max()) + 1e-300
+        if E is not None:
+            if free.any():
+                nu = np.linalg.lstsq(E[:, free].T, g0[free], rcond=None)[0]
+                g0 = g0 - E.T @ nu
+        l0 = np.where(free, np.abs(g0), 0.0)
+        l0 = np.maximum(l0, np.where(at_lo & ~at_hi & ~pinned, np.maximum(-g0, 0.0), 0.0))
+        l0 = np.maximum(l0, np.where(at_hi & ~at_lo & ~pinned, np.maximum(g0, 0.0), 0.0))
+        level0 = max(level0, float((l0 / s0).max()))
+        pinned = pinned | (~free & (np.abs(g0) > 1e-7 * s0))  # this level holds these at their bound
+        E = Al if E is None else np.concatenate([E, Al], axis=0)
     G = A0 @ M
     timp = _tau_imp(prob, inp, b)
     r = np.linalg.solve(M, x - timp) if prob.joint_weight == 0 else x - timp

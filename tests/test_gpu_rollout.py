@@ -150,3 +150,53 @@ def test_rollout_config4_full_size_properties(wbq_mod, oracle_lib):
     for b in sorted(check):
         c = kkt.qppvm_certificate(oracle_lib, prob, last, b, tau[b])
         assert max(c["primal"], c["level0"], c["stat"], c["sign"]) <= 1e-9, (b, c)
+
+
+@pytest.mark.parametrize("plant", [False, True])
+def test_rollout_paths_agree(wbq_mod, plant):
+    """The execution paths of a rollout give the same answer (include/wbq.h wbq_set_option): one
+    launch for the whole rollout (qppvm_rollout_kernel, the default), one launch per step with the
+    level-0 repair inline in the fast kernel, and one launch per step with the repair in its own
+    kernel. plant=False is the SURVEY 8d distribution, where most instance-steps go through the
+    level-0 repair (bench.py --mpc-inputs survey), so every path's repair runs; the statuses and
+    warm-start hints agree exactly, the torques and states to roundoff."""
+    n, B, H, dt = 30, 256, 8, 1e-3
+    inp = qppvm_instances(QPPVMProblem(n=n), B, seed=21, plant=plant)
+    free = wbq_mod.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B)
+    tau_free, _, _ = free.solve_batch(inp)
+    free.close()
+    prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(tau_free), 0.8)))
+    out = {}
+    for name, fused, inl in (("fused", 1, -1), ("steps_inline", 0, 1), ("steps_kernel", 0, 0)):
+        s = wbq_mod.QPPVMSolver(prob, max_batch=B)
+        try:
+            s.set_option(s.OPT_FUSED_ROLLOUT, fused)
+            s.set_option(s.OPT_INLINE_REPAIR, inl)
+            s.set_inputs(inp)
+            s.rollout(H, dt)
+            tau, st, _ = s.outputs()
+            q, qd = s.state()
+            out[name] = (tau, st, q, qd, s.warm_hints())
+        finally:
+            s.close()
+    tau0, st0, q0, qd0, h0 = out["fused"]
+    if not plant:
+        assert h0.sum() > B // 4  # the repair path carries many of the rollouts
+    for name in ("steps_inline", "steps_kernel"):
+        tau, st, q, qd, h = out[name]
+        np.testing.assert_array_equal(st, st0, err_msg=name)
+        np.testing.assert_array_equal(h, h0, err_msg=name)
+        assert rel_err(tau, tau0) <= 1e-9, (name, rel_err(tau, tau0))
+        assert rel_err(q, q0) <= 1e-12 and rel_err(qd, qd0) <= 1e-10, name
+
+
+def test_set_option_rejects_bad_values(wbq_mod):
+    s = wbq_mod.QPPVMSolver(QPPVMProblem(n=30), max_batch=4)
+    try:
+        with pytest.raises(wbq_mod.WbqError):
+            s.set_option(s.OPT_INLINE_REPAIR, 2)
+        with pytest.raises(wbq_mod.WbqError):
+            s.set_option(99, 0)
+        s.set_option(s.OPT_FUSED_ROLLOUT, 0)
+    finally:
+        s.close()

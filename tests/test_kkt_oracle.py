@@ -73,3 +73,30 @@ def test_friction_lsi_certificate_and_reference(oracle_lib, mu):
         yr = inp["Jw"][b] @ x_r[b, :n]
         assert np.abs(y - yr).max() <= 1e-6 * max(1.0, np.abs(yr).max()), (b, np.abs(y - yr).max())
     assert faces_held > 0  # the pyramid really binds in this sweep
+
+
+@pytest.mark.parametrize("n,q", [(14, 0.6), (20, 0.3), (30, 0.5)])
+def test_three_level_certificate_accepts_oracle(oracle_lib, n, q):
+    """The elbow level (task_level (0, 0, 1, 1): ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint,
+    QPPVMPlugin.cpp:154-166,177-178): the oracle's lexicographic chain (level-0 BVLS, the middle level
+    by BVLS in the null space of the level-0 rows, oracle/wbq_oracle.c:wbq_ref_level_mid, the joint
+    task last) carries the three-level certificate, and differs from the two-level stack that sums
+    the four tasks where the limits bind; the two-level answer fails the three-level certificate."""
+    rm = (7, 7, 7, 7)
+    free = QPPVMProblem(n=n, ntasks=4, row_mask=rm, tau_max=1e9)
+    inp = qppvm_instances(free, 32, seed=31 + n)
+    t0, _, _ = oracle_lib.qppvm_batch(free, inp)
+    tm = float(np.quantile(np.abs(t0), q))
+    p3 = QPPVMProblem(n=n, ntasks=4, row_mask=rm, tau_max=tm, task_level=(0, 0, 1, 1))
+    p2 = QPPVMProblem(n=n, ntasks=4, row_mask=rm, tau_max=tm)
+    t3, s3, _ = oracle_lib.qppvm_batch(p3, inp)
+    t2, s2, _ = oracle_lib.qppvm_batch(p2, inp)
+    assert (s3 == 0).all() and (s2 == 0).all()
+    cs = [kkt.qppvm_certificate(oracle_lib, p3, inp, b, t3[b]) for b in range(32)]
+    ok = worst(cs, ("primal", "level0", "stat", "sign"))
+    assert max(ok.values()) <= TOL, ok
+    differ = np.abs(t3 - t2).max(axis=1) > 1e-6 * np.abs(t2).max(axis=1)
+    if n < 30:
+        assert differ.sum() >= 4
+        bad = [kkt.qppvm_certificate(oracle_lib, p3, inp, b, t2[b])["level0"] for b in np.where(differ)[0]]
+        assert max(bad) > 1e-6
