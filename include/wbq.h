@@ -118,7 +118,7 @@ typedef struct {
      *   ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits  = task_level {0, 0, 1, 1}.
      * The middle level is lexicographic: min ||A1 x - b1||^2 keeping level 0 at its optimum y0*, and
      * the joint task then keeps both. All zero (a zero-initialised tail): the reference stack.
-     * Needs W1 = I and n <= 32 (else wbq_create returns WBQ_E_UNSUPPORTED). */
+     * Needs W1 = I and at most 6 rows per level (else wbq_create returns WBQ_E_UNSUPPORTED). */
     int task_level[4];
 } wbq_desc;
 

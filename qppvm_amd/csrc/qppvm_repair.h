@@ -53,7 +53,9 @@ struct PivChol {
         return v;
     }
 
-    __device__ void factor(const double (&g)[T], int m, double tol)
+    // pivots at or below tol * (largest diagonal), and below `floor` (absolute: a matrix that is zero
+    // up to roundoff has rank 0, which a relative cut alone would not see), end the factorisation
+    __device__ void factor(const double (&g)[T], int m, double tol, double floor = 0.0)
     {
         double d[K], dmx = 0.0;
 #pragma unroll
@@ -79,7 +81,7 @@ struct PivChol {
                     best = d[i];
                     p = i;
                 }
-            stop = stop || !(best > tol * dmx);
+            stop = stop || !(best > tol * dmx) || !(best > floor);
             if (!stop) {
                 piv[c] = p;
                 k = c + 1;
@@ -380,6 +382,201 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
     return out;
 }
 
+// BVLS with equality rows (the middle level of a three-level stack, wbq_desc.task_level: the elbow
+// tasks of QPPVMPlugin.cpp:154-166,177-178; the oracle's wbq_ref_level_mid states the same steps with
+// SVDs):
+//   min 0.5 ||A1 z - b1||^2  s.t.  A0 z = A0 z_start (level 0 at its optimum),  lo <= z <= hi,
+// from a feasible z_start (the level-0 point) with box state st0. Lane i owns variable z_i with its
+// level-0 column ae (me rows) and level-1 column ao (mo rows). A free-set step keeps A0_F dz = 0: with
+// Q0 = A0_F^T L^-T (PivChol<ME>::basis on each lane's own column; orthonormal basis of range(A0_F^T))
+// and T = Q0^T A1_F^T, the projected level-1 Gram is S = K11 - T^T T, beta = S^+ r1 and
+//   dz_j = a1_j . beta - q0_j . (T beta)  (= (P A1^T beta)_j, P = I - Q0 Q0^T),
+// interpolated back into the box as BVLS; the multipliers of bound variables are
+//   w_j = a1_j . r1 - (A0^T nu)_j,  A0_F^T nu = Q0 Q0^T g_F  =>  (A0^T nu)_j = qe_j . (Q0^T g_F),
+// qe_j = L^-1 of lane j's own level-0 column (every lane, bound or free).
+struct BvlsEqOut {
+    double xv, w; // z_i and its final multiplier w_i (a bound variable held by it: |w_i| large)
+    int st, it;
+    bool capped;
+};
+template <int NP, int ME, int MO>
+__device__ __forceinline__ BvlsEqOut bvls_eq(const double (&ae)[ME], int me, const double (&ao)[MO], const double (&bo)[MO],
+                                             int mo, double lo, double hi, bool row, bool active, double x0, int st0,
+                                             int maxit)
+{
+    constexpr int TE = ME * (ME + 1) / 2, TO = MO * (MO + 1) / 2;
+    const int i = threadIdx.x & (NP - 1); // lane within the instance
+    BvlsEqOut out{0.0, 0.0, 0, 0, false};
+    double xv = row ? fmin(fmax(x0, lo), hi) : 0.0;
+    int st = row ? st0 : 2;
+    if (row && lo == hi) st = -1;
+    if (st == -1) xv = lo;
+    if (st == 1) xv = hi;
+    bool ex = false;
+    double abm = 0.0;
+#pragma unroll
+    for (int c = 0; c < MO; ++c) abm = fma(ao[c], bo[c], abm);
+    const double wtb = fabs(abm);
+    abm = fmax(1.0, imax<NP>(wtb));
+    int freed = -1, it = 0;
+    // the free set's projection: qe = L^-1 of this lane's level-0 column (PivChol of K00 = A0_F A0_F^T),
+    // T = Q0^T A1_F^T, S = K11 - T^T T; k11d the diagonal of K11
+    auto project = [&](bool fr, double (&qe)[ME], double (&S)[TO], double (&Tm)[ME][MO], double &k11max) {
+        double k00[TE], k11[TO];
+#pragma unroll
+        for (int p = 0; p < ME; ++p)
+#pragma unroll
+            for (int c = 0; c <= p; ++c) k00[tri(p, c)] = fr ? ae[p] * ae[c] : 0.0;
+#pragma unroll
+        for (int p = 0; p < MO; ++p)
+#pragma unroll
+            for (int c = 0; c <= p; ++c) k11[tri(p, c)] = fr ? ao[p] * ao[c] : 0.0;
+        isum_vec<NP, TE>(k00);
+        isum_vec<NP, TO>(k11);
+        PivChol<ME> pe;
+        pe.factor(k00, me, 1e-12);
+        pe.basis(ae, qe);
+        double tv[ME * MO];
+#pragma unroll
+        for (int p = 0; p < ME; ++p)
+#pragma unroll
+            for (int c = 0; c < MO; ++c) tv[p * MO + c] = fr ? qe[p] * ao[c] : 0.0;
+        isum_vec<NP, ME * MO>(tv);
+        k11max = 0.0;
+#pragma unroll
+        for (int p = 0; p < ME; ++p)
+#pragma unroll
+            for (int c = 0; c < MO; ++c) Tm[p][c] = tv[p * MO + c];
+#pragma unroll
+        for (int p = 0; p < MO; ++p) {
+            k11max = fmax(k11max, k11[tri(p, p)]);
+#pragma unroll
+            for (int c = 0; c <= p; ++c) {
+                double v = k11[tri(p, c)];
+#pragma unroll
+                for (int e = 0; e < ME; ++e) v = fma(-Tm[e][p], Tm[e][c], v);
+                S[tri(p, c)] = v;
+            }
+        }
+    };
+    bool outer = active;
+    while (__any(outer)) {
+        bool inner = outer;
+        while (__any(inner)) {
+            if (inner) ++it;
+            const bool fr = inner && row && st == 0;
+            const double kfree = isum<NP>(fr ? 1.0 : 0.0);
+            double qe[ME], S[TO], Tm[ME][MO], k11max;
+            project(fr, qe, S, Tm, k11max);
+            double rv[MO];
+#pragma unroll
+            for (int c = 0; c < MO; ++c) rv[c] = row ? ao[c] * xv : 0.0;
+            isum_vec<NP, MO>(rv);
+#pragma unroll
+            for (int c = 0; c < MO; ++c) rv[c] = bo[c] - rv[c];
+            PivChol<MO> ps;
+            ps.factor(S, mo, 1e-12, 1e-12 * k11max);
+            double beta[MO], tb[ME];
+            ps.solve(rv, mo, beta);
+#pragma unroll
+            for (int e = 0; e < ME; ++e) {
+                double v = 0.0;
+#pragma unroll
+                for (int c = 0; c < MO; ++c) v = fma(Tm[e][c], beta[c], v);
+                tb[e] = v;
+            }
+            double dz = 0.0;
+            if (fr) {
+#pragma unroll
+                for (int c = 0; c < MO; ++c) dz = fma(ao[c], beta[c], dz);
+#pragma unroll
+                for (int e = 0; e < ME; ++e) dz = fma(-qe[e], tb[e], dz);
+            }
+            double al = kInf;
+            if (fr) {
+                const double zt = xv + dz;
+                if (zt < lo && dz < 0.0) al = fmax(0.0, (lo - xv) / dz);
+                else if (zt > hi && dz > 0.0) al = fmax(0.0, (hi - xv) / dz);
+                if (!(al < 1.0)) al = kInf;
+            }
+            int jb = i;
+            iargmin<NP>(al, jb);
+            if (inner) {
+                if (!(kfree > 0.0) || ps.k == 0) { // no direction left on the free set
+                    inner = false;
+                } else if (al >= kInf) { // the step stays in the box: take it
+                    if (fr) xv += dz;
+                    freed = -1;
+                    ex = false;
+                    inner = false;
+                } else {
+                    const double alpha = fmax(al, 0.0);
+                    if (jb == freed && alpha == 0.0) { // Stark-Parker: re-bind the variable just freed
+                        if (i == jb) {
+                            ex = true;
+                            st = dz < 0.0 ? -1 : 1;
+                            xv = st < 0 ? lo : hi;
+                        }
+                        inner = false;
+                    } else {
+                        ex = false;
+                        if (fr) {
+                            xv = fma(alpha, dz, xv);
+                            if (i == jb) st = dz < 0.0 ? -1 : 1;
+                            if (st == -1) xv = lo;
+                            if (st == 1) xv = hi;
+                        }
+                    }
+                    freed = -1;
+                    if (it >= maxit) inner = false;
+                }
+            }
+        }
+        // multipliers of the bound variables: w = a1 . r1 - (A0^T nu)
+        const bool fr = row && st == 0;
+        double qe[ME], S[TO], Tm[ME][MO], k11max;
+        project(fr, qe, S, Tm, k11max);
+        double rv[MO];
+#pragma unroll
+        for (int c = 0; c < MO; ++c) rv[c] = row ? ao[c] * xv : 0.0;
+        isum_vec<NP, MO>(rv);
+        double g = 0.0, wx = 0.0;
+#pragma unroll
+        for (int c = 0; c < MO; ++c) {
+            g = fma(ao[c], bo[c] - rv[c], g);
+            wx = fma(ao[c], rv[c], wx);
+        }
+        double qg[ME];
+#pragma unroll
+        for (int e = 0; e < ME; ++e) qg[e] = fr ? qe[e] * g : 0.0;
+        isum_vec<NP, ME>(qg);
+        double w = g;
+#pragma unroll
+        for (int e = 0; e < ME; ++e) w = fma(-qe[e], qg[e], w);
+        out.w = row ? w : 0.0;
+        const double wtol = 1e-11 * fmax(abm, imax<NP>(fmax(wtb, fabs(wx))));
+        double v = -kInf;
+        if (outer && row && (st == -1 || st == 1) && !ex && lo != hi) v = st < 0 ? w : -w;
+        int best = i;
+        iargmax<NP>(v, best);
+        if (outer) {
+            if (!(v > wtol)) {
+                outer = false;
+            } else if (it >= maxit) {
+                out.capped = true;
+                outer = false;
+            } else {
+                if (i == best) st = 0; // exclusions persist until the inner loop makes progress
+                freed = best;
+            }
+        }
+    }
+    out.xv = xv;
+    out.st = st;
+    out.it = it;
+    return out;
+}
+
 struct RepairOut {
     double lo, hi, u; // (possibly pinned) limits and the new u of this lane
     double x;         // the BVLS point x* of this lane (level 0 in x-space)
@@ -458,9 +655,17 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     for (int c = 0; c < M0; ++c) abm = fma(acol[c], b0v[c], abm);
     abm = fmax(1.0, imax<NP>(fabs(abm)));
     const double pintol = 1e-9 * abm;
-    const BvlsOut bv = bvls<NP, M0>(acol, b0v, m0, lo, hi, row, rep, st0, 50 * n + 100);
-    const double xv = bv.xv;
-    const int st = bv.st, it = bv.it;
+    // level-0 rows: all m0 of them, or the first a.m_l0 when a middle level follows (task_level)
+    const int ml = (M0 > 6 && a.m_l0 > 0 && a.m_l0 < m0) ? a.m_l0 : m0;
+    double acol0[M0], b0v0[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        acol0[c] = c < ml ? acol[c] : 0.0;
+        b0v0[c] = c < ml ? b0v[c] : 0.0;
+    }
+    const BvlsOut bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100);
+    double xv = bv.xv;
+    int st = bv.st, it = bv.it;
     if (bv.capped) out.status = 1;
     WBQ_STAMP(10);
     // ---- y* = A0 x*, pins, and the least-distance point of G u = y*
@@ -469,6 +674,50 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
 #pragma unroll
     for (int c = 0; c < M0; ++c) ys[c] = acol[c] * xv;
     isum_vec<NP, M0>(ys);
+    if constexpr (M0 > 6) {
+        if (ml < m0) {
+            // the middle level (the elbow tasks, QPPVMPlugin.cpp:154-166,177-178): level-0 pins first,
+            // then min ||A1 x - b1|| keeping A0 x = y0* (bvls_eq), its own pins, and y1* = A1 x1*
+            double l0w = 0.0;
+#pragma unroll
+            for (int c = 0; c < M0; ++c) l0w = fma(acol0[c], b0v0[c] - ys[c], l0w);
+            double lo1 = lo, hi1 = hi;
+            if (row && l0w > pintol) lo1 = hi;
+            else if (row && l0w < -pintol) hi1 = lo;
+            double ae[6], ao[6], bo[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                ae[c] = c < ml ? acol[c] : 0.0;
+                double v = 0.0, bb = 0.0;
+#pragma unroll
+                for (int r = 0; r < M0; ++r) {
+                    v = (r == ml + c) ? acol[r] : v;
+                    bb = (r == ml + c) ? b0v[r] : bb;
+                }
+                ao[c] = (ml + c < m0) ? v : 0.0;
+                bo[c] = (ml + c < m0) ? bb : 0.0;
+            }
+            double abm1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) abm1 = fma(ao[c], bo[c], abm1);
+            abm1 = fmax(1.0, imax<NP>(row ? fabs(abm1) : 0.0));
+            const BvlsEqOut be = bvls_eq<NP, 6, 6>(ae, ml, ao, bo, m0 - ml, lo1, hi1, row, rep, xv, st, 50 * n + 100);
+            xv = be.xv;
+            it += be.it;
+            if (be.capped) out.status = 1;
+            // the variables the middle level's multipliers hold at a bound (level-0 pins stay)
+            if (row && lo1 != hi1 && be.st == -1 && be.w < -1e-9 * abm1) hi1 = lo1;
+            if (row && lo1 != hi1 && be.st == 1 && be.w > 1e-9 * abm1) lo1 = hi1;
+            lo = lo1;
+            hi = hi1;
+            double y1[M0];
+#pragma unroll
+            for (int c = 0; c < M0; ++c) y1[c] = acol[c] * xv;
+            isum_vec<NP, M0>(y1);
+#pragma unroll
+            for (int c = 0; c < M0; ++c) ys[c] = c < ml ? ys[c] : y1[c];
+        }
+    }
     {
         double gap = 0.0, bmx = 1.0;
 #pragma unroll
@@ -481,9 +730,11 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     if (row) {
         double w = 0.0;
 #pragma unroll
-        for (int c = 0; c < M0; ++c) w = fma(acol[c], b0v[c] - ys[c], w);
-        if (w > pintol) out.lo = hi;       // pinned at the upper bound
-        else if (w < -pintol) out.hi = lo; // pinned at the lower bound
+        for (int c = 0; c < M0; ++c) w = fma(acol0[c], b0v0[c] - ys[c], w);
+        out.lo = lo; // (with a middle level: its pins and level 0's already in lo / hi)
+        out.hi = hi;
+        if (w > pintol) out.lo = out.hi;       // pinned at the upper bound
+        else if (w < -pintol) out.hi = out.lo; // pinned at the lower bound
     }
     out.x = row ? xv : 0.0;
     // Level 1 keeps A0 x = y* and the (pinned) box. When the columns of A0 over the variables

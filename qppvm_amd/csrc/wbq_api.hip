@@ -32,6 +32,7 @@ struct wbq_ctx {
     int nfield = 0;            // fp64 input fields and their elements per instance
     size_t fe[16] = {};
     int m0 = 0;
+    int m_l0 = 0; // level-0 rows (m0 but with a middle level, task_level)
     int limits_crossed = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -290,18 +291,31 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     if (d.joint_weight != WBQ_WEIGHT_IDENTITY && d.joint_weight != WBQ_WEIGHT_INERTIA) return WBQ_E_INVALID;
     if (!d.Kc || !d.Dc || !d.Kq || !d.Dq || !d.tau_max || !d.tau_min) return WBQ_E_INVALID;
     if (d.joint_limits && (!d.q_min || !d.q_max || !d.Kjl || !d.Djl)) return WBQ_E_INVALID;
-    int m0 = 0;
+    int m0 = 0, m_l0 = 0;
     int sel[wbq::kM0Max];
+    bool mid = false;
     for (int t = 0; t < d.ntasks; ++t) {
+        if (d.task_level[t] != 0 && d.task_level[t] != 1) return WBQ_E_INVALID;
+        mid |= d.task_level[t] == 1;
+    }
+    // the task rows, level 0's first, then the middle level's (task_level)
+    for (int tt = 0; tt < 2 * d.ntasks; ++tt) {
+        const int t = tt % d.ntasks;
+        if ((d.task_level[t] != 0) != (tt >= d.ntasks)) continue;
         if (d.row_mask[t] <= 0 || d.row_mask[t] >= 64) return WBQ_E_INVALID;
         for (int r = 0; r < 6; ++r)
             if ((d.row_mask[t] >> r) & 1) {
                 if (m0 == wbq::kM0Max) return WBQ_E_UNSUPPORTED;
+                if (tt < d.ntasks) ++m_l0;
                 sel[m0++] = t * 6 + r;
             }
     }
     // W1 = M runs the active set in constraint space, one lane per level-0 row and torque limit
     if (d.joint_weight == WBQ_WEIGHT_INERTIA && m0 + d.n > 64) return WBQ_E_UNSUPPORTED;
+    // a middle level: at least one task on level 0, W1 = I (the u-space repair carries the middle
+    // step), at most 6 rows per level (the repair's 6-row bvls_eq blocks)
+    if (mid && (m_l0 == 0 || d.joint_weight != WBQ_WEIGHT_IDENTITY || m_l0 > 6 || m0 - m_l0 > 6))
+        return WBQ_E_UNSUPPORTED;
     wbq_ctx *c = new wbq_ctx();
     c->d = d;
     c->d.Kc = c->d.Dc = c->d.Kq = c->d.Dq = c->d.tau_max = c->d.tau_min = nullptr;
@@ -309,6 +323,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     c->d.joint_limits = d.joint_limits ? 1 : 0;
     if (c->d.max_iter <= 0) c->d.max_iter = 4 * d.n + 32;
     c->m0 = m0;
+    c->m_l0 = m_l0;
     c->device = device;
     for (int j = 0; j < d.n; ++j)
         if (d.tau_min[j] > d.tau_max[j]) c->limits_crossed = 1;
@@ -571,6 +586,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.n = c->d.n;
     a.ntasks = c->d.ntasks;
     a.m0 = c->m0;
+    a.m_l0 = c->m_l0;
     a.select_mode = c->d.select_mode;
     a.joint_weight = c->d.joint_weight;
     a.max_iter = c->d.max_iter;
@@ -678,7 +694,7 @@ int wbq_rollout(wbq_ctx *c, int steps, double dt)
     // QPPVM W1 = I with n <= 32 and m0 <= 6: the whole rollout in one launch (qppvm_rollout_kernel);
     // WBQ_OPT_FUSED_ROLLOUT = 0 keeps one launch per step (the A/B of the two)
     if (c->opt_fused && steps > 0 && c->form == WBQ_FORM_QPPVM && c->d.joint_weight == WBQ_WEIGHT_IDENTITY &&
-        c->d.n <= 32 && c->m0 <= 6)
+        c->d.n <= 32 && c->m0 <= 6 && c->m_l0 == c->m0)
         return solve_impl(c, 1, dt, false, nullptr, steps);
     for (int k = 0; k < steps; ++k) {
         const int rc = solve_impl(c, 1, dt);

@@ -45,7 +45,8 @@ struct QppvmArgs {
     int B;           // instances
     int n;           // joints (<= NP of the instantiation)
     int ntasks;      // Cartesian tasks
-    int m0;          // level-0 rows (selected task rows)
+    int m0;          // Cartesian rows (selected task rows of every task)
+    int m_l0;        // of them level 0's (the first m_l0); the rest a middle level (wbq_desc task_level)
     int select_mode; // WBQ_SELECT_*
     int joint_weight; // WBQ_WEIGHT_*: W1 = I (qppvm_kernel.hip) or W1 = M (qppvm_w1m_kernel.hip)
     int max_iter;    // active-set step cap

@@ -60,3 +60,19 @@ def load_golden_contact(n, fname=None):
                               tau_max=z[pre + "tau_max"], **ext)
         inp = {k: np.ascontiguousarray(z[pre + k]) for k in CONTACT_INPUT_FIELDS}
         yield g, prob, inp, {"tau": z[pre + "tau"], "x": z[pre + "x"]}
+
+
+def load_golden_elbow():
+    """Yield (group, QPPVMProblem, inputs, expected) of the three-level stack fixtures
+    (tests/golden/qppvm_elbow.npz, make_golden_elbow.py): task_level (0, 0, 1, 1), the elbow level of
+    QPPVMPlugin.cpp:154-166,177-178."""
+    from qppvm_amd.problem import QPPVMProblem
+    z = np.load(os.path.join(GOLDEN, "qppvm_elbow.npz"))
+    for g in z["groups"]:
+        g = str(g)
+        pre = g + "__"
+        prob = QPPVMProblem(n=int(z[pre + "n"]), ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1),
+                            tau_max=z[pre + "tau_max"])
+        inp = {k: np.ascontiguousarray(z[pre + k]) for k in INPUT_KEYS}
+        exp = {k: z[pre + k] for k in ("tau", "y", "kat") if pre + k in z}
+        yield g, prob, inp, exp

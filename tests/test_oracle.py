@@ -77,3 +77,21 @@ def test_infeasible_bounds_fallback(oracle_lib):
     tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
     assert np.all(st == 2)
     np.testing.assert_array_equal(tau, inp["h"])
+
+
+def test_oracle_three_level_golden(oracle_lib):
+    """The oracle's lexicographic three-level chain (task_level: the elbow level between the hands and
+    the joint task, QPPVMPlugin.cpp:154-166,177-178) against the independent numpy/scipy fixtures
+    (tests/golden/make_golden_elbow.py), including the groups where the elbow level is not attained."""
+    from conftest import load_golden_elbow, rel_err
+    seen_unattained = 0
+    for g, prob, inp, exp in load_golden_elbow():
+        tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
+        assert (st == 0).all(), g
+        assert rel_err(tau, exp["tau"]) <= 1e-8, (g, rel_err(tau, exp["tau"]))
+        if "kat" in exp:
+            assert rel_err(tau, exp["kat"]) <= 1e-8, g
+        for b in range(tau.shape[0]):
+            a = oracle_lib.assemble(prob, inp, b)
+            seen_unattained += np.abs(exp["y"][b][6:] - a["b0"][6:]).max() > 1e-6 * max(1, np.abs(a["b0"]).max())
+    assert seen_unattained >= 4  # the middle level binds in the fixtures
