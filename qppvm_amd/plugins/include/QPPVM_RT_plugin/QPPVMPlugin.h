@@ -40,6 +40,11 @@ public:
     // the JointLimits constraint the reference builds and comments out of its stack (:169-173):
     // set before init_control_plugin
     void set_joint_limits(bool on) { _use_joint_limits = on; }
+    // the elbow tasks the reference builds (:154-166, on arm1_4 / arm2_4) and leaves commented out of
+    // its stack (:177-178), as a middle level: ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits.
+    // Set before init_control_plugin
+    void set_elbow_level(bool on) { _use_elbow = on; }
+    int ntasks() const { return (int)_ee_links.size(); }
     const Eigen::VectorXd &joint_limit(int which) const { return which ? _q_max : _q_min; }
     const Eigen::VectorXd &joint_limit_gain(int which) const { return which ? _d_jl : _k_jl; }
     // the Cartesian references the tasks track (t = 0 right, 1 left): the on_start poses, the
@@ -56,8 +61,10 @@ private:
     XBot::ModelInterface::Ptr _model;
     wbq_ctx *_ctx = nullptr;
 
-    // task wiring (QPPVMPlugin.cpp:129-152): right arm then left arm, as in the stack sum
+    // task wiring (QPPVMPlugin.cpp:129-152): right arm then left arm, as in the stack sum; with the
+    // elbow level the elbow tasks follow (:154-166: left, then right, as in :178's sum)
     std::vector<std::string> _ee_links{"arm2_7", "arm1_7"};
+    bool _use_elbow = false;
     double _start_time = 0.0;
     int _status = 0;
     int _iters = 0;
@@ -65,7 +72,7 @@ private:
 
     Eigen::VectorXd _q, _dq, _q_ref, _q_home, _k, _d, _tau_d, _h, _tau_qp;
     Eigen::VectorXd _tau_max_const, _tau_min_const;
-    Eigen::Affine3d _ee_ref[2];
+    std::vector<Eigen::Affine3d> _ee_ref = std::vector<Eigen::Affine3d>(2);
     // _set_ref: left end-effector reference on a circle in the y-z plane (:217-223), on the
     // reference's KDL frames (QPPVMPlugin.h:98-99)
     bool _set_ref = false;

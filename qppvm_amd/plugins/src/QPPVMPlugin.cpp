@@ -64,13 +64,21 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle) // :42-199
     // :148-149); rows {0,1,2} (:134, :147); ((ee_right + ee_left) / joint) << limits (:177-179);
     // QPOases_sot(.., 1.0) (:188)
     const int n = _model->getJointNum();
-    const Eigen::VectorXd Kc = Eigen::VectorXd::Constant(12, 700.0), Dc = Eigen::VectorXd::Constant(12, 70.0);
+    if (_use_elbow) _ee_links = {"arm2_7", "arm1_7", "arm1_4", "arm2_4"}; // :129-166
+    const int T = (int)_ee_links.size();
+    _ee_ref.resize((size_t)T);
+    // the elbow tasks' gains are OpenSoT's defaults in the reference (never set, :154-166;
+    // [upstream], not pinnable offline): the hands' 700 / 70 here
+    const Eigen::VectorXd Kc = Eigen::VectorXd::Constant(6 * T, 700.0), Dc = Eigen::VectorXd::Constant(6 * T, 70.0);
     const Eigen::VectorXd Kq = Eigen::VectorXd::Constant(n, 5.0), Dq = Eigen::VectorXd::Constant(n, 2.0);
     wbq_desc d{};
     d.form = WBQ_FORM_QPPVM;
     d.n = n;
-    d.ntasks = 2;
-    d.row_mask[0] = d.row_mask[1] = 0x7;
+    d.ntasks = T;
+    for (int t = 0; t < T; ++t) {
+        d.row_mask[t] = 0x7;                  // OpenSoT::Indices::range(0,2) (:134, :147, :158, :165)
+        d.task_level[t] = t < 2 ? 0 : 1;      // the elbows below the hands (:177-178)
+    }
     d.select_mode = WBQ_SELECT_SUBTASK;
     d.joint_weight = WBQ_WEIGHT_IDENTITY;
     d.max_batch = 1;
@@ -103,9 +111,9 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle) // :42-199
     _matlogger->createVectorVariable("tau_desired", n, 1, 30000);
     _matlogger->createScalarVariable("time_matlogger", 1, 30000);
     _M.resize((size_t)n * n);
-    _J.resize((size_t)2 * 6 * n);
-    _pose.resize(24);
-    _pose_ref.resize(24);
+    _J.resize((size_t)T * 6 * n);
+    _pose.resize((size_t)12 * T);
+    _pose_ref.resize((size_t)12 * T);
     return true;
 }
 
@@ -126,6 +134,7 @@ void QPPVMPlugin::on_start(double time) // :261-305
     _model->getPose(_ee_links[0], right_ee_pose);
     _ee_ref[1] = left_ee_pose;
     _ee_ref[0] = right_ee_pose;
+    for (size_t t = 2; t < _ee_links.size(); ++t) _model->getPose(_ee_links[t], _ee_ref[t]); // the elbows
     _q_ref = _q;
 
     _model->getPose(_ee_links[1], _start_pose); // :287
@@ -147,7 +156,7 @@ void QPPVMPlugin::QPPVMControl(const double time) // :201-259
     // the ABI's row-major layout (include/wbq.h; Eigen's MatrixXd is column-major)
     _model->getInertiaMatrix(_Mtmp);
     copy_row_major(_Mtmp, n, n, _M.data());
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < (int)_ee_links.size(); ++t) {
         _model->getJacobian(_ee_links[t], _Jtmp);
         copy_row_major(_Jtmp, 6, n, _J.data() + (size_t)t * 6 * n);
         Eigen::Affine3d P;

@@ -98,7 +98,7 @@ int main(int argc, char **argv)
 {
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
-    bool forceacc = false, stress = false, set_ref = false, joint_limits = false;
+    bool forceacc = false, stress = false, set_ref = false, joint_limits = false, elbow = false;
     int wd = 3;
     double mu = 0.0;
     const char *log_prefix = nullptr;
@@ -109,6 +109,7 @@ int main(int argc, char **argv)
         else if (!std::strcmp(argv[k], "--stress")) stress = true;
         else if (!std::strcmp(argv[k], "--set-ref")) set_ref = true; // QPPVMPlugin.cpp:217-223
         else if (!std::strcmp(argv[k], "--joint-limits")) joint_limits = true; // :169-171
+        else if (!std::strcmp(argv[k], "--elbow")) elbow = true;               // :154-166, :177-178
         else if (!std::strcmp(argv[k], "--wrench6")) wd = 6;                   // ForceAcc.cpp:67
         else if (!std::strcmp(argv[k], "--mu") && k + 1 < argc) mu = std::atof(argv[++k]);
         else if (!std::strcmp(argv[k], "--log") && k + 1 < argc) log_prefix = argv[++k];
@@ -122,12 +123,16 @@ int main(int argc, char **argv)
     dummy::Params prm;
     prm.n = n;
     if (stress) prm.jscale = 0.5;
+    const std::vector<std::string> links = elbow ? std::vector<std::string>{"arm2_7", "arm1_7", "arm1_4", "arm2_4"}
+                                                 : std::vector<std::string>{"arm2_7", "arm1_7"};
+    prm.links = links;
     auto handle = std::make_shared<dummy::Handle>(prm);
     handle->register_model();
     demo::QPPVMPlugin plugin;
     if (log_prefix) plugin.set_log_prefix(log_prefix);
     plugin.set_reference_trajectory(set_ref);
     plugin.set_joint_limits(joint_limits);
+    plugin.set_elbow_level(elbow);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;
@@ -136,13 +141,13 @@ int main(int argc, char **argv)
     const double dt = 1e-3;
     plugin.on_start(0.0);
     if (f) {
-        // header: n, ticks, then the references fixed at on_start (q_ref, pose_ref x2)
-        const int hdr[2] = {n, dump_ticks};
-        std::fwrite(hdr, sizeof(int), 2, f);
+        // header: n, ticks, tasks, then the references fixed at on_start (q_ref, pose_ref per task)
+        const int hdr[3] = {n, dump_ticks, (int)links.size()};
+        std::fwrite(hdr, sizeof(int), 3, f);
         Eigen::VectorXd q;
         handle->model().getJointPosition(q);
         std::fwrite(q.data(), sizeof(double), n, f);
-        for (const char *link : {"arm2_7", "arm1_7"}) {
+        for (const std::string &link : links) {
             Eigen::Affine3d P;
             double pm[12];
             handle->model().getPose(link, P);
@@ -182,12 +187,12 @@ int main(int argc, char **argv)
             std::vector<double> rm((size_t)6 * n > (size_t)n * n ? (size_t)6 * n : (size_t)n * n);
             copy_row_major(M, n, n, rm.data());
             std::fwrite(rm.data(), sizeof(double), (size_t)n * n, f);
-            for (const char *link : {"arm2_7", "arm1_7"}) {
+            for (const std::string &link : links) {
                 m.getJacobian(link, J);
                 copy_row_major(J, 6, n, rm.data());
                 std::fwrite(rm.data(), sizeof(double), (size_t)6 * n, f);
             }
-            for (const char *link : {"arm2_7", "arm1_7"}) {
+            for (const std::string &link : links) {
                 Eigen::Affine3d P;
                 double pm[12];
                 m.getPose(link, P);

@@ -19,16 +19,16 @@ TOL = 1e-6
 
 def read_dump(path):
     raw = open(path, "rb").read()
-    n, ticks = np.frombuffer(raw[:8], dtype=np.int32)
-    off = 8
+    n, ticks, T = (int(v) for v in np.frombuffer(raw[:12], dtype=np.int32))
+    off = 12
     f64 = lambda k: np.frombuffer(raw[off:off + 8 * k], dtype=np.float64)  # noqa: E731
     qref = f64(n).copy(); off += 8 * n
-    pose_ref = f64(24).copy(); off += 8 * 24
+    pose_ref = f64(12 * T).copy(); off += 8 * 12 * T
     rec = {k: [] for k in ("M", "J", "pose", "q", "qd", "h", "tau", "status")}
     for _ in range(ticks):
         rec["M"].append(f64(n * n).reshape(n, n)); off += 8 * n * n
-        rec["J"].append(f64(12 * n).reshape(2, 6, n)); off += 8 * 12 * n
-        rec["pose"].append(f64(24)); off += 8 * 24
+        rec["J"].append(f64(6 * T * n).reshape(T, 6, n)); off += 8 * 6 * T * n
+        rec["pose"].append(f64(12 * T)); off += 8 * 12 * T
         for k in ("q", "qd", "h", "tau"):
             rec[k].append(f64(n)); off += 8 * n
         rec["status"].append(int(np.frombuffer(raw[off:off + 4], dtype=np.int32)[0])); off += 4
@@ -217,3 +217,30 @@ def test_forceacc_matlogger(tmp_path):
     f = d["x"][:, n:].reshape(20, nc, 3)
     tau_c = np.einsum("bckn,bck->bn", d["Jc"][:, :, :3, :], f)
     np.testing.assert_allclose(m["tau_c"][:, :20].T, tau_c, rtol=1e-12, atol=1e-9)
+
+
+def test_dummy_driver_elbow_level(tmp_path, oracle_lib):
+    """The elbow toggle of the QPPVM shell: the elbow tasks the reference builds on arm1_4 / arm2_4
+    (QPPVMPlugin.cpp:154-166) as the middle level its commented stack line puts them on (:177-178),
+    ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits. Every dumped tick re-solved by the
+    oracle's three-level chain; the nominal and the stress plant (level-0 repairs on every tick)."""
+    from qppvm_amd import build
+    driver = build.build_plugins()[1]
+    for stress in (False, True):
+        dump = str(tmp_path / f"dump_elbow{int(stress)}.bin")
+        r = subprocess.run([driver, "--ticks", "200", "--dump", dump, "40", "--elbow"] + (["--stress"] if stress else []),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        n, d = read_dump(dump)
+        assert d["J"].shape[1] == 4
+        prob = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1))
+        inp = {k: np.ascontiguousarray(d[k]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
+        tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+        np.testing.assert_array_equal(d["status"], st_r)
+        ok = st_r == 0
+        assert ok.sum() >= len(ok) - 2
+        assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, (stress, rel_err(d["tau"][ok], tau_r[ok]))
+        if stress:  # the elbow level changes the torques against the reference's two-level stack
+            two = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7))
+            tau_2, _, _ = oracle_lib.qppvm_batch(two, inp)
+            assert rel_err(tau_2, d["tau"]) > 1e-6
