@@ -411,7 +411,10 @@ def cpu_baseline_threads(form, prob, inp, budget_s):
         done = sum(ex.map(worker, range(T)))
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "QP-solves/s", "cores": T, "kind": "port",
-            "sample": f"{done} instances in {dt:.1f} s, {T} threads, one instance stream each"}
+            "sample": f"{done} instances in {dt:.1f} s, {T} threads, one instance stream each",
+            "cores_note": "threads = min(16, affinity): 16 is this job's CPU share on the GPU box (one GPU's "
+                          "slice of the host); nproc / lscpu report the whole host, whose other cores belong "
+                          "to other jobs, so an all-host-cores run is not available to this process"}
 
 
 def host_cpu():

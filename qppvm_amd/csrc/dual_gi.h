@@ -382,10 +382,18 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
             return true;
         }
     }
-    // truncate back to the k0 slots
+    // truncate back to the k0 slots: the slot state of lanes k0.. returns to its defaults too (every
+    // reader masks by g.k, but no rejected row may linger in act / sgn / lam / aeq)
     Trow.zero_if(i >= k0);
     Tcol.zero_from(k0);
     GA.zero_from(k0);
+    if (i >= k0) {
+        const GiState d0;
+        g.act = d0.act;
+        g.sgn = d0.sgn;
+        g.lam = d0.lam;
+        g.aeq = d0.aeq;
+    }
     S[V.AC + i] = (double)g.act;
     __syncthreads();
     return false;

@@ -228,6 +228,57 @@ struct PivChol {
     }
 };
 
+// w = Gram^-1 r by an unpivoted Cholesky of the leading m x m block of a packed PSD Gram (every lane
+// alike, static indices: ~K^3 / 6 FMAs instead of PivChol's select chains). Returns false -- w
+// untouched -- unless every pivot exceeds tol * (largest diagonal): then the Gram is far from
+// singular, no rank decision is needed, and the caller's PivChol path (the same solution for a full
+// rank Gram) is skipped. The BVLS steps of the level-0 repair are mostly such full-rank solves.
+template <int K>
+__device__ __forceinline__ bool chol_solve_full(const double (&g)[K * (K + 1) / 2], int m, const double (&r)[K],
+                                                double (&w)[K], double tol)
+{
+    double L[K * (K + 1) / 2], il[K], dmx = 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < K; ++c) dmx = fmax(dmx, c < m ? g[tri(c, c)] : 0.0);
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        double dd = c < m ? g[tri(c, c)] : 1.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) dd = fma(-L[tri(c, k)], L[tri(c, k)], dd);
+        ok = ok && (c >= m || dd > tol * dmx);
+        const double ic = c < m ? frsq(fmax(dd, 1e-300)) : 0.0;
+        il[c] = ic;
+        L[tri(c, c)] = dd * ic;
+#pragma unroll
+        for (int rr = c + 1; rr < K; ++rr) {
+            double t = (rr < m && c < m) ? g[tri(rr, c)] : 0.0;
+#pragma unroll
+            for (int k = 0; k < c; ++k) t = fma(-L[tri(rr, k)], L[tri(c, k)], t);
+            L[tri(rr, c)] = t * ic;
+        }
+    }
+    if (!ok || !(dmx > 0.0)) return false;
+    double y[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        double v = c < m ? r[c] : 0.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) v = fma(-L[tri(c, k)], y[k], v);
+        y[c] = v * il[c];
+    }
+#pragma unroll
+    for (int c = K - 1; c >= 0; --c) {
+        double v = y[c];
+#pragma unroll
+        for (int k = c + 1; k < K; ++k) v = fma(-L[tri(k, c)], y[k], v);
+        y[c] = v * il[c];
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) w[c] = c < m ? y[c] : 0.0;
+    return true;
+}
+
 template <int NP, int K>
 __device__ __forceinline__ void isum_vec(double (&v)[K])
 {
@@ -291,9 +342,10 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             const double kfree = isum<NP>(fr ? 1.0 : 0.0);
 #pragma unroll
             for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
-            // minimum-norm least squares on the free set: z = A_F^T w
+            // minimum-norm least squares on the free set: z = A_F^T w (a full-rank Gram by the plain
+            // Cholesky, a nearly singular one by the rank-revealing PivChol)
             double wv[M0];
-            {
+            if (!chol_solve_full<M0>(gp, m0, rv, wv, 1e-10)) {
                 PivChol<M0> pc;
                 pc.factor(gp, m0, 1e-12);
                 pc.solve(rv, m0, wv);

@@ -120,7 +120,10 @@ def lsi_certificate(A0, bb, z, lo, hi, groups=(), mu=0.0, act_tol=1e-8):
     v = np.where(~(at_lo | at_hi), np.abs(w), 0.0)
     v = np.maximum(v, np.where(at_lo & ~at_hi, np.maximum(w, 0.0), 0.0))
     v = np.maximum(v, np.where(at_hi & ~at_lo, np.maximum(-w, 0.0), 0.0))
-    primal = max(0.0, (lo - z).max(initial=0.0), (z - hi).max(initial=0.0))
+    with np.errstate(invalid="ignore"):
+        pl = np.where(np.isfinite(lo), (lo - z) / (1.0 + np.abs(np.where(np.isfinite(lo), lo, 0.0))), 0.0)
+        ph = np.where(np.isfinite(hi), (z - hi) / (1.0 + np.abs(np.where(np.isfinite(hi), hi, 0.0))), 0.0)
+    primal = max(0.0, pl.max(initial=0.0), ph.max(initial=0.0))  # relative to the bound
     for j in groups:
         from scipy.optimize import nnls
         fv, wc = z[j:j + 3], w[j:j + 3]
@@ -166,33 +169,41 @@ def contact_level0_certificate(oracle, prob, inp, b, x):
 
 def contact_certificate(oracle, prob, inp, b, x, waist=None):
     """Scaled residuals of instance b's contact-form output x = [qdd; f]; waist (optional) replaces
-    the waist target b_w (level 1 after a level-0 repair keeps J_w qdd = y0*)."""
+    the waist target b_w (level 1 after a level-0 repair keeps J_w qdd = y0*).
+
+    No activity threshold decides which rows the multipliers may use (round 3 classified rows as
+    active at a relative slack of 1e-8, the kernel's own re-check tolerance): every inequality row
+    within 1e-6 of a bound is a candidate in the least-squares fit H x + g = E^T nu + C^T mu, and a
+    multiplier on a row that is not exactly at its bound is charged through complementarity,
+    |mu_j| / max|mu| * slack_j (a row 1e-7 off its bound carrying a full-size multiplier fails). Signs
+    (mu >= 0 at clo, <= 0 at chi) are checked where the candidate normals are independent (the
+    multipliers are unique there). Keys: primal, stat (fit residual), sign (worst wrong-signed
+    multiplier, scaled), comp (complementarity), indep."""
     a = oracle.contact_assemble(prob, inp, b)
     H, g, E, e, C, clo, chi = a["H"], a["g"], a["E"], a["e"], a["C"], a["clo"], a["chi"]
     if waist is not None:
         e = e.copy()
         e[:6] = waist
     cx = C @ x
-    scale = 1.0 + max(np.abs(e).max(), np.abs(np.concatenate([clo, chi])[np.isfinite(np.concatenate([clo, chi]))]).max(initial=0.0))
+    fin = np.concatenate([clo, chi])
+    scale = 1.0 + max(np.abs(e).max(), np.abs(fin[np.abs(fin) < 1e299]).max(initial=0.0))
     primal = max(np.abs(E @ x - e).max(), max(0.0, (clo - cx).max(initial=0.0), (cx - chi).max(initial=0.0))) / scale
-    # a row met to 1e-8 relative is active: the dual loop accepts its active rows at that level
-    # (qppvm_amd/csrc/dual_gi.h, the final re-check)
-    at_lo, at_hi = _active(cx, clo, chi, 1e-8)
-    act = np.where(at_lo | at_hi)[0]
-    K = np.concatenate([E.T, C[act].T], axis=1)
+    rs = 1.0 + np.abs(cx)
+    s_lo, s_hi = (cx - clo) / rs, (chi - cx) / rs  # relative slacks (huge for an unbounded side)
+    cand = np.where((s_lo <= 1e-6) | (s_hi <= 1e-6))[0]
+    K = np.concatenate([E.T, C[cand].T], axis=1)
     r = H @ x + g
     lam, *_ = np.linalg.lstsq(K, r, rcond=None)
     stat = float(np.abs(r - K @ lam).max() / (np.abs(H @ x).max() + np.abs(g).max() + 1e-300))
     indep = np.linalg.matrix_rank(K, tol=1e-10 * np.abs(K).max()) == K.shape[1]
+    mu = lam[E.shape[0]:]
+    mscale = np.abs(lam).max() + 1e-300
+    near_lo = s_lo[cand] <= s_hi[cand]
+    slack = np.where(near_lo, s_lo[cand], s_hi[cand])
+    comp = float((np.abs(mu) / mscale * np.maximum(slack, 0.0)).max(initial=0.0))
     sign = 0.0
     if indep:
-        mu = lam[E.shape[0]:]
-        mscale = np.abs(lam).max() + 1e-300
-        for c, j in enumerate(act):
-            if clo[j] == chi[j]:
-                continue
-            if at_lo[j] and not at_hi[j]:
-                sign = max(sign, -mu[c] / mscale)
-            elif at_hi[j] and not at_lo[j]:
-                sign = max(sign, mu[c] / mscale)
-    return dict(primal=primal, stat=stat, sign=sign, indep=bool(indep))
+        eq = clo[cand] == chi[cand]
+        wrong = np.where(near_lo, -mu, mu) / mscale
+        sign = float(np.where(eq, 0.0, np.maximum(wrong, 0.0)).max(initial=0.0))
+    return dict(primal=primal, stat=stat, sign=sign, comp=comp, indep=bool(indep))

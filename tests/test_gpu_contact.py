@@ -123,7 +123,7 @@ def test_contact_level0_repair(wbq_mod, oracle_lib):
         for b in np.where(~solved & (st == 0))[0]:
             l0, y = kkt.contact_level0_certificate(oracle_lib, prob, inp, b, x[b])
             c = kkt.contact_certificate(oracle_lib, prob, inp, b, x[b], waist=y)
-            assert l0 <= 1e-9 and max(c["primal"], c["stat"], c["sign"]) <= 1e-9, (seed, b, l0, c)
+            assert l0 <= 1e-9 and max(c["primal"], c["stat"], c["sign"], c["comp"]) <= 1e-9, (seed, b, l0, c)
     assert tot["repaired"] >= 100, tot  # the repair path really runs
     assert tot["miss"] <= MAX_MISS, tot
 

@@ -52,17 +52,25 @@ def run_churn(wbq_mod, Solver, prob, inp, alt, calls=4):
         warm.close()
 
 
-@pytest.mark.parametrize("torque_rows", [False, True])
-def test_contact_warm_equals_cold(wbq_mod, torque_rows):
-    free = ContactProblem(n=30, nc=4)
-    inp = contact_instances(free, 512, seed=1, masks=MASKS)
-    alt = contact_instances(free, 512, seed=2, masks=MASKS)
+@pytest.mark.parametrize("torque_rows,nc,wd,mu", [(False, 4, 3, 0.0), (True, 4, 3, 0.0),
+                                                   (False, 2, 6, 0.0), (False, 4, 6, 0.0),
+                                                   (False, 2, 3, 0.4), (False, 4, 3, 0.4),
+                                                   (False, 2, 6, 0.4), (True, 2, 6, 0.5), (True, 4, 3, 0.4)])
+def test_contact_warm_equals_cold(wbq_mod, torque_rows, nc, wd, mu):
+    """Every contact-form variant the shapes select (register slots, LDS slots with one-sided friction
+    faces, 6-D wrench boxes, torque rows): dual_gi.h warm_extend over repeated solves on one context
+    gives the cold answer."""
+    free = ContactProblem(n=30, nc=nc, wrench_dim=wd, mu=mu)
+    masks = MASKS if nc == 4 else None
+    inp = contact_instances(free, 512, seed=1, masks=masks)
+    alt = contact_instances(free, 512, seed=2, masks=masks)
     prob = free
     if torque_rows:
         s = wbq_mod.ContactSolver(free, max_batch=512)
         tf, _, _ = s.solve_batch(inp)
         s.close()
-        prob = ContactProblem(n=30, nc=4, torque_rows=True, tau_max=float(np.quantile(np.abs(tf[:, 6:]), 0.85)))
+        prob = ContactProblem(n=30, nc=nc, wrench_dim=wd, mu=mu, torque_rows=True,
+                              tau_max=float(np.quantile(np.abs(tf[:, 6:]), 0.85)))
     saved = 0
     for tw, sw, iw, tc, sc, ic, pick in run_churn(wbq_mod, wbq_mod.ContactSolver, prob, inp, alt):
         np.testing.assert_array_equal(sw, sc)

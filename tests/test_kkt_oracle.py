@@ -38,7 +38,7 @@ def test_contact_certificate_accepts_oracle_and_rejects_perturbed(oracle_lib):
     inp = contact_instances(prob, 16, seed=12, masks=[0b0011, 0b0111, 0b1111])
     _, x, st, _, _ = oracle_lib.contact_batch(prob, inp)
     ok = worst([kkt.contact_certificate(oracle_lib, prob, inp, b, x[b]) for b in range(16) if st[b] == 0],
-               ("primal", "stat", "sign"))
+               ("primal", "stat", "sign", "comp"))
     assert max(ok.values()) <= TOL, ok
     bad = [kkt.contact_certificate(oracle_lib, prob, inp, b, x[b] * (1 + 1e-6)) for b in range(8)]
     assert all(max(c["primal"], c["stat"]) > 1e-9 for c in bad)
