@@ -859,6 +859,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
         __syncthreads();
     }
+    WBQ_STAMP(9); // (diagnostic build: the equality batch ends here)
     if constexpr (!REPAIR) { // the last solve's active inequality rows on top (dual_gi.h warm_extend)
         if (gs.status == 0 && a.ws_rows) {
             const int wsg = kind == 2 ? (int)a.ws_rows[b * 64 + i] : 0;

@@ -898,8 +898,10 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             int st2 = 0, it2 = 0;
             bool inf = false;
             const int wsg = (ga && warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
+            WBQ_STAMP(18); // (diagnostic build: the inline dual active set starts)
             const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
                                                true);
+            WBQ_STAMP(19);
             const bool rep = active && (inf || to_rep);
             if (active && !rep) { // (before the repair below, which reuses the wave's LDS)
                 double tau2 = x2 + h_i;

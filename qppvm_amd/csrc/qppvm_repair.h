@@ -715,7 +715,18 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         acol0[c] = c < ml ? acol[c] : 0.0;
         b0v0[c] = c < ml ? b0v[c] : 0.0;
     }
-    const BvlsOut bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100);
+    BvlsOut bv;
+    if (M0 > 6 && ml <= 6) { // (a middle level: level 0 has at most 6 rows, the 6-row BVLS suffices)
+        double a6[6], b6[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            a6[c] = acol0[c < M0 ? c : 0];
+            b6[c] = b0v0[c < M0 ? c : 0];
+        }
+        bv = bvls<NP, 6>(a6, b6, ml, lo, hi, row, rep, st0, 50 * n + 100);
+    } else {
+        bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100);
+    }
     double xv = bv.xv;
     int st = bv.st, it = bv.it;
     if (bv.capped) out.status = 1;

@@ -41,7 +41,8 @@ def run(prob, inp, reps=10):
             "active_set_cycles_per_step": float((d[:, 4] / steps).mean()),
             "steps_mean_max": [float(iters.mean()), int(iters.max())],
             "refine_rounds_mean": float(full[:, 7].mean()),
-            "split_active_set": {"warm/equality batch": float((full[:, 8] - full[:, 4]).mean()),
+            "split_active_set": {"equality batch": float((full[:, 9] - full[:, 4]).mean()),
+                                 "warm extend": float((full[:, 8] - full[:, 9]).mean()),
                                  "dual loop + rebuild + refinement": float((full[:, 5] - full[:, 8]).mean())},
             "status_ok": float((status == 0).mean())}
 

@@ -42,13 +42,17 @@ def run(libpath, prob, inp, reps=20, stamps=False):
         out["fast_kernel_phase_cycles_mean"]["(stage: wait for M + Y)"] = float((full[:, 1] - full[:, 15]).mean())
         out["fast_block_cycles_p50_p90"] = [float(np.percentile(st[:, -1] - st[:, 0], q)) for q in (50, 90)]
         rt = full[:, 16:18]  # s_memrealtime (100 MHz, global): start / end offsets in us
+        rt = rt[(rt[:, 0] > 0) & (rt[:, 1] >= rt[:, 0])]  # blocks that wrote both stamps
         t0 = rt[:, 0].min()
         out["fast_block_start_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 0] - t0, q)) / 100 for q in (10, 50, 90, 100)]
         out["fast_block_end_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 1] - t0, q)) / 100 for q in (10, 50, 90, 100)]
         out["fast_block_dur_us_p10_p50_p90_max"] = [float(np.percentile(rt[:, 1] - rt[:, 0], q)) / 100 for q in (10, 50, 90, 100)]
         # by XCD (round-robin block dispatch: XCD = block id % 8)
         xcd = np.arange(nb) % 8
-        out["fast_block_dur_us_mean_by_xcd"] = [float((rt[xcd == x, 1] - rt[xcd == x, 0]).mean()) / 100 for x in range(8)]
+        rtf = full[:, 16:18]
+        okr = (rtf[:, 0] > 0) & (rtf[:, 1] >= rtf[:, 0])
+        out["fast_block_dur_us_mean_by_xcd"] = [float((rtf[okr & (xcd == x), 1] - rtf[okr & (xcd == x), 0]).mean()) / 100
+                                                for x in range(8)]
         out["fast_block_cycles_mean_by_xcd"] = [float((st[xcd == x, -1] - st[xcd == x, 0]).mean()) for x in range(8)]
         _, status, iters = s.outputs()
         it_blk = iters[: 2 * nb].reshape(nb, -1).max(axis=1) if nb < B else iters[:nb]
@@ -62,6 +66,11 @@ def run(libpath, prob, inp, reps=20, stamps=False):
             out["active_cycles_per_step_mean"] = float((loop / it_blk[act]).mean())
             out["active_block_max_steps_p50_p90_max"] = [float(np.percentile(it_blk[act], q)) for q in (50, 90, 100)]
             out["iters_hist"] = np.bincount(iters).tolist()
+        inl = full[:, 19] > full[:, 18]  # NP = 32: the inline dual active set (stamps 18 / 19)
+        if inl.any():
+            c = full[inl, 19] - full[inl, 18]
+            out["inline_active_blocks"] = int(inl.sum())
+            out["inline_active_cycles_p50_p90_max"] = [float(np.percentile(c, q)) for q in (50, 90, 100)]
         rep = full[:, 12] > full[:, 8]
         if rep.any():
             r = full[rep][:, 8:13]

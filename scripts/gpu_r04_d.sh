@@ -11,3 +11,8 @@ timeout -k 10 300 qppvm_amd/qppvm_dummy_driver --ticks 10000 --stress > gpurun_o
 tail -n 1 gpurun_out/dummy_stress.log
 timeout -k 10 300 qppvm_amd/qppvm_dummy_driver --ticks 10000 > gpurun_out/dummy_nominal.log 2>&1 || exit 1
 tail -n 1 gpurun_out/dummy_nominal.log
+timeout -k 10 300 python scripts/ab_rollout.py > gpurun_out/ab_rollout.log 2>&1 || exit 1
+cat gpurun_out/ab_rollout.log
+timeout -k 10 300 python scripts/diag_phases.py > gpurun_out/diag_phases.log 2>&1 || exit 1
+timeout -k 10 300 python scripts/diag_contact.py > gpurun_out/diag_contact.log 2>&1 || exit 1
+echo diag done
