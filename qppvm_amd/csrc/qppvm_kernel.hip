@@ -445,15 +445,9 @@ __device__ double minv_apply(const QppvmArgs &a, double *S, const ActiveLayout<N
 {
     const int n = a.n;
     const int ic = i < n ? i : n - 1;
-    const double *Mb = a.M + b * n * n + ic; // (64-bit addressing: instances from a work list)
-    double A[NP];
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
-#pragma unroll
-    for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     double rhs[1] = {row ? x : 0.0};
     __syncthreads();
-    (void)block_gj<NP, 1, 1>(A, rhs, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
+    minv_rows<NP, 1>(a.M + b * n * n + ic, n, i, row, rhs, S + L.QA, S + L.QA + 2 * kGjBS * NP);
     return rhs[0];
 }
 
@@ -580,7 +574,15 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int T = a.ntasks, n = a.n, m0 = a.m0;
     const FastLayout<NP> L(T, m0);
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;
+    // (a rollout step: the lane index is opaque per step, or the loop-invariant values derived from it
+    // -- the identity padding of M, LDS offsets -- are hoisted out of the step loop and spilled across
+    // every step. With this and the opaque arguments below: 1,504 -> 560 B of scratch, the hot path's
+    // scratch loads per step ~240 -> ~60, and a repair-free 4096 x 20 rollout 1.45 -> 0.75 ms, the
+    // time of 20 separate launches, 0.71 ms. (Putting the inline repair behind a noinline call as well
+    // removed the rest of the hot path's spills, but the kernel then faulted on MI355X with an illegal
+    // memory access even where no repair ran: not used.))
+    if constexpr (ROLL) asm volatile("" : "+v"(tid));
     const int sub = tid / NP;
     const int i = tid - sub * NP;
     const long b = (long)blockIdx.x * IPW + sub;
@@ -977,7 +979,13 @@ __global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
     }
 #pragma unroll 1
     for (int s = 0; s < a.steps; ++s) {
-        fast_body<NP, M0, true, TM, 2, 32, true, true>(a);
+        // the arguments through an opaque kernarg pointer per step: values loaded from them are not
+        // hoisted out of the loop and spilled (1,504 -> 1,056 B of scratch with this alone)
+        typedef const __attribute__((address_space(4))) char *KPtr;
+        KPtr kp = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const QppvmArgs &as = *(const QppvmArgs *)(const char *)kp;
+        fast_body<NP, M0, true, TM, 2, 32, true, true>(as);
         __syncthreads(); // this wave's q, qd and warm-start writes are visible to its next step
     }
 }

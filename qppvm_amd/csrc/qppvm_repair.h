@@ -629,6 +629,35 @@ __device__ __forceinline__ BvlsEqOut bvls_eq(const double (&ae)[ME], int me, con
     return out;
 }
 
+// rhs <- M^-1 rhs (lane i: row i of the NR right-hand sides) by block Gauss-Jordan on M's rows reloaded
+// from HBM/L2 (the rare paths; Mb = this lane's column of its instance's M, 64-bit addressing: the
+// instances of a wave come from a work list). NC = the columns held per lane: 40 when n <= 40 in 64
+// lanes (the n = 39 CENTAURO size), as the fast kernel's MR -- 24 fewer columns to update and 48 fewer
+// VGPRs than NP (the repair kernels' Gauss-Jordan spilled at NC = 64).
+template <int NP, int NR, int NC>
+__device__ __forceinline__ void minv_rows_nc(const double *Mb, int n, int i, bool row, double (&rhs)[NR], double *PN,
+                                             double *RH)
+{
+    double A[NC];
+#pragma unroll
+    for (int r = 0; r < NC; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
+#pragma unroll
+    for (int r = 0; r < NC; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+    (void)block_gj<NP, NR, NR, NC>(A, rhs, n, i, PN, RH);
+}
+template <int NP, int NR>
+__device__ __forceinline__ void minv_rows(const double *Mb, int n, int i, bool row, double (&rhs)[NR], double *PN,
+                                          double *RH)
+{
+    if constexpr (NP == 64) {
+        if (n <= 40) {
+            minv_rows_nc<NP, NR, 40>(Mb, n, i, row, rhs, PN, RH);
+            return;
+        }
+    }
+    minv_rows_nc<NP, NR, NP>(Mb, n, i, row, rhs, PN, RH);
+}
+
 struct RepairOut {
     double lo, hi, u; // (possibly pinned) limits and the new u of this lane
     double x;         // the BVLS point x* of this lane (level 0 in x-space)
@@ -672,17 +701,8 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     }
     // a_i = row i of M^-1 G^T: Gauss-Jordan on the M rows (QA region as scratch; the Q1 rows
     // are rebuilt below)
-    {
-        // 64-bit addressing: the instances of a wave come from a work list (no uniform base)
-        const double *Mb = a.M + b * n * n + ic;
-        double A[NP];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = Mb[(r < n ? r : n - 1) * n];
-#pragma unroll
-        for (int r = 0; r < NP; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
-        __syncthreads();
-        (void)block_gj<NP, M0, M0>(A, acol, n, i, S + L.QA, S + L.QA + 2 * kGjBS * NP);
-    }
+    __syncthreads();
+    minv_rows<NP, M0>(a.M + b * n * n + ic, n, i, row, acol, S + L.QA, S + L.QA + 2 * kGjBS * NP);
     WBQ_STAMP(9);
     // ---- BVLS (oracle/wbq_oracle.c:wbq_ref_level0); warm start (any state is valid): the bound
     // SET of the last repair, each variable on the side the level-0 gradient at that corner

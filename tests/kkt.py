@@ -173,12 +173,13 @@ def contact_certificate(oracle, prob, inp, b, x, waist=None):
 
     No activity threshold decides which rows the multipliers may use (round 3 classified rows as
     active at a relative slack of 1e-8, the kernel's own re-check tolerance): every inequality row
-    within 1e-6 of a bound is a candidate in the least-squares fit H x + g = E^T nu + C^T mu, and a
+    within a window (1e-9 .. 1e-6, the best of the four kept) of a bound is a candidate in the
+    least-squares fit H x + g = E^T nu + C^T mu, and a
     multiplier on a row that is not exactly at its bound is charged through complementarity,
     |mu_j| / max|mu| * slack_j (a row 1e-7 off its bound carrying a full-size multiplier fails). Signs
     (mu >= 0 at clo, <= 0 at chi) are checked where the candidate normals are independent (the
     multipliers are unique there). Keys: primal, stat (fit residual), sign (worst wrong-signed
-    multiplier, scaled), comp (complementarity), indep."""
+    multiplier, scaled), comp (complementarity), indep, window."""
     a = oracle.contact_assemble(prob, inp, b)
     H, g, E, e, C, clo, chi = a["H"], a["g"], a["E"], a["e"], a["C"], a["clo"], a["chi"]
     if waist is not None:
@@ -190,20 +191,29 @@ def contact_certificate(oracle, prob, inp, b, x, waist=None):
     primal = max(np.abs(E @ x - e).max(), max(0.0, (clo - cx).max(initial=0.0), (cx - chi).max(initial=0.0))) / scale
     rs = 1.0 + np.abs(cx)
     s_lo, s_hi = (cx - clo) / rs, (chi - cx) / rs  # relative slacks (huge for an unbounded side)
-    cand = np.where((s_lo <= 1e-6) | (s_hi <= 1e-6))[0]
-    K = np.concatenate([E.T, C[cand].T], axis=1)
     r = H @ x + g
-    lam, *_ = np.linalg.lstsq(K, r, rcond=None)
-    stat = float(np.abs(r - K @ lam).max() / (np.abs(H @ x).max() + np.abs(g).max() + 1e-300))
-    indep = np.linalg.matrix_rank(K, tol=1e-10 * np.abs(K).max()) == K.shape[1]
-    mu = lam[E.shape[0]:]
-    mscale = np.abs(lam).max() + 1e-300
-    near_lo = s_lo[cand] <= s_hi[cand]
-    slack = np.where(near_lo, s_lo[cand], s_hi[cand])
-    comp = float((np.abs(mu) / mscale * np.maximum(slack, 0.0)).max(initial=0.0))
-    sign = 0.0
-    if indep:
-        eq = clo[cand] == chi[cand]
-        wrong = np.where(near_lo, -mu, mu) / mscale
-        sign = float(np.where(eq, 0.0, np.maximum(wrong, 0.0)).max(initial=0.0))
-    return dict(primal=primal, stat=stat, sign=sign, comp=comp, indep=bool(indep))
+    rscale = np.abs(H @ x).max() + np.abs(g).max() + 1e-300
+    best = None
+    # KKT asks for SOME multipliers: every candidate window is tried and the best certificate kept
+    # (on a degenerate instance the min-norm fit over the widest window spreads weight onto rows that
+    # are slightly off their bound, which a narrower window does not offer it)
+    for win in (1e-9, 1e-8, 1e-7, 1e-6):
+        cand = np.where((s_lo <= win) | (s_hi <= win))[0]
+        K = np.concatenate([E.T, C[cand].T], axis=1)
+        lam, *_ = np.linalg.lstsq(K, r, rcond=None)
+        stat = float(np.abs(r - K @ lam).max() / rscale)
+        indep = np.linalg.matrix_rank(K, tol=1e-10 * np.abs(K).max()) == K.shape[1]
+        mu = lam[E.shape[0]:]
+        mscale = np.abs(lam).max() + 1e-300
+        near_lo = s_lo[cand] <= s_hi[cand]
+        slack = np.where(near_lo, s_lo[cand], s_hi[cand])
+        comp = float((np.abs(mu) / mscale * np.maximum(slack, 0.0)).max(initial=0.0))
+        sign = 0.0
+        if indep:
+            eq = clo[cand] == chi[cand]
+            wrong = np.where(near_lo, -mu, mu) / mscale
+            sign = float(np.where(eq, 0.0, np.maximum(wrong, 0.0)).max(initial=0.0))
+        c = dict(primal=primal, stat=stat, sign=sign, comp=comp, indep=bool(indep), window=win)
+        if best is None or max(stat, sign, comp) < max(best["stat"], best["sign"], best["comp"]):
+            best = c
+    return best
