@@ -207,7 +207,7 @@ __device__ __forceinline__ LsiOut fric_lsi(const double (&acol)[M0], const doubl
 #pragma unroll
             for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
             double wv[M0];
-            if (!chol_solve_full<M0>(gp, m0, rv, wv, 1e-10)) {
+            if (!chol_solve_full<M0>(gp, m0, rv, wv, kCholFastTol<M0>)) {
                 PivChol<M0> pc;
                 pc.factor(gp, m0, 1e-12);
                 pc.solve(rv, m0, wv);

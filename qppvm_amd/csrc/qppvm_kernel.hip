@@ -475,9 +475,14 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     const bool uniq = ro.unique;
     const ActiveLayout<NP> L(a.ntasks, a.m0);
     double x_i = ro.x;
+    // the dual active set starts from the BVLS point's bound set in one batch (gi_solve's warm start:
+    // kept only if independent and dual feasible, else cold; the path changes, never the solution). The
+    // level-1 optimum keeps level 0 at y*, so its active bounds are mostly those BVLS ended on: a config-4
+    // rollout's repaired instance-steps took up to ~90 cold steps (scripts/diag_mpc_steps.py)
+    const int wsr = (row && !uniq) ? -ro.st : 0; // gi_solve's sides: +1 lower, -1 upper
     if (__any(rep && !uniq))
         x_i = gi_solve<NP, M0>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
-                               infeasible);
+                               infeasible, wsr, true);
     if (uniq) x_i = ro.x;
     if (a.integrate && __any(rep && uniq)) { // rollouts integrate qdd = u = M^-1 x*
         const bool r2 = row && uniq;
@@ -501,7 +506,8 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     if (rep && (i & (NP - 1)) == 0) {
         a.status[b] = status;
         a.iters[b] = iters + ro.it;
-        a.ws_hint[b] = ro.l0inf ? 1 : 0;
+        // bit 1: ws_rows holds this solve's final bound set (the dual active set ran and ended well)
+        a.ws_hint[b] = (ro.l0inf ? 1 : 0) | ((!uniq && status == 0) ? 2 : 0);
     }
 }
 

@@ -279,6 +279,16 @@ __device__ __forceinline__ bool chol_solve_full(const double (&g)[K * (K + 1) / 
     return true;
 }
 
+// Acceptance threshold of chol_solve_full's pivots (relative to the largest diagonal). It must be far
+// above PivChol's rank cut (1e-12): an unpivoted pivot bounds the smallest eigenvalue only up to a factor
+// that grows with K, so a Gram whose unpivoted pivots all pass 1e-10 can still be rank deficient to the
+// pivoted factorisation, and the plain solve then takes a huge ill-conditioned step where PivChol takes
+// the minimum-norm one. With 1e-10 a W1 = M config-2 instance's BVLS cycled to its cap and returned a
+// wrong y* (tests/test_gpu_kkt.py; replayed in numpy: 1,600 steps vs 26, y* off by 2 %); at 1e-6 (1e-4 for
+// 12 rows) the fast path only takes Grams PivChol also finds well inside full rank.
+template <int K>
+constexpr double kCholFastTol = K <= 6 ? 1e-6 : 1e-4;
+
 template <int NP, int K>
 __device__ __forceinline__ void isum_vec(double (&v)[K])
 {
@@ -345,7 +355,7 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             // minimum-norm least squares on the free set: z = A_F^T w (a full-rank Gram by the plain
             // Cholesky, a nearly singular one by the rank-revealing PivChol)
             double wv[M0];
-            if (!chol_solve_full<M0>(gp, m0, rv, wv, 1e-10)) {
+            if (!chol_solve_full<M0>(gp, m0, rv, wv, kCholFastTol<M0>)) {
                 PivChol<M0> pc;
                 pc.factor(gp, m0, 1e-12);
                 pc.solve(rv, m0, wv);
@@ -662,6 +672,7 @@ struct RepairOut {
     double lo, hi, u; // (possibly pinned) limits and the new u of this lane
     double x;         // the BVLS point x* of this lane (level 0 in x-space)
     int status, it;   // status 1 if BVLS hit its cap; BVLS iterations
+    int st;           // this lane's final BVLS state (-1 at lo, +1 at hi, 0 free or padding)
     bool l0inf;       // y* != b0: level 0 really is infeasible at b0 (warm-start hint)
     bool unique;      // the level-1 feasible set is the single point x*: level 1 has nothing left
 };
@@ -688,7 +699,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     const int n = a.n, m0 = a.m0;
     const int ic = i < n ? i : n - 1;
     const bool row = rep && i < n;
-    RepairOut out{lo, hi, 0.0, 0.0, 0, 0, false, false};
+    RepairOut out{lo, hi, 0.0, 0.0, 0, 0, 0, false, false};
     double gcol[M0], acol[M0], b0v[M0];
     const double uimp = rep ? a.ui_scr[b * NP + i] : 0.0;
 #pragma unroll
@@ -786,6 +797,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
             abm1 = fmax(1.0, imax<NP>(row ? fabs(abm1) : 0.0));
             const BvlsEqOut be = bvls_eq<NP, 6, 6>(ae, ml, ao, bo, m0 - ml, lo1, hi1, row, rep, xv, st, 50 * n + 100);
             xv = be.xv;
+            st = be.st;
             it += be.it;
             if (be.capped) out.status = 1;
             // the variables the middle level's multipliers hold at a bound (level-0 pins stay)
@@ -820,6 +832,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         else if (w < -pintol) out.hi = out.lo; // pinned at the lower bound
     }
     out.x = row ? xv : 0.0;
+    out.st = (row && (st == -1 || st == 1)) ? st : 0;
     // Level 1 keeps A0 x = y* and the (pinned) box. When the columns of A0 over the variables
     // left free are independent, x_F is fixed by A0_F x_F = y* - A0_P x_P: the feasible set is
     // the single point x* and the level-1 objective cannot move it (the generic saturated case:
