@@ -289,14 +289,6 @@ __device__ __forceinline__ bool chol_solve_full(const double (&g)[K * (K + 1) / 
 template <int K>
 constexpr double kCholFastTol = K <= 6 ? 1e-6 : 1e-4;
 
-template <int NP, int K>
-__device__ __forceinline__ void isum_vec(double (&v)[K])
-{
-#pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1)
-#pragma unroll
-        for (int c = 0; c < K; ++c) v[c] += __shfl_xor(v[c], m, NP);
-}
 
 // BVLS (Stark-Parker; the algorithm of oracle/wbq_oracle.c:wbq_ref_level0) on
 //   min 0.5 ||A z - b||^2  s.t.  lo <= z <= hi
@@ -309,7 +301,15 @@ struct BvlsOut {
     double xv;
     int st, it;
     bool capped;
+#ifdef WBQ_STAMPS
+    unsigned long long ph[8]; // diagnostic build: cycles in the step's parts, fast / pivoted solves
+#endif
 };
+#ifdef WBQ_STAMPS
+#define WBQ_T(v) do { __builtin_amdgcn_sched_barrier(0); v = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define WBQ_T(v) do {} while (0)
+#endif
 template <int NP, int M0>
 __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (&b0v)[M0], int m0, double lo,
                                         double hi, bool row, bool active, int st0, int maxit)
@@ -317,6 +317,12 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
     constexpr int NT = M0 * (M0 + 1) / 2;
     const int i = threadIdx.x & (NP - 1); // lane within the instance
     BvlsOut out{0.0, 0, 0, false};
+#ifdef WBQ_STAMPS
+    for (int k = 0; k < 8; ++k) out.ph[k] = 0;
+#endif
+    unsigned long long t0 = 0, t1 = 0;
+    (void)t0;
+    (void)t1;
     double xv = row ? fmin(fmax(0.0, lo), hi) : 0.0;
     int st = row ? 0 : 2; // 0 free, -1 at lo, +1 at hi, 2 padding lane (never free)
     if (row && st0 != 0) {
@@ -339,6 +345,7 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
         bool inner = outer;
         while (__any(inner)) {
             if (inner) ++it;
+            WBQ_T(t0);
             const bool fr = inner && st == 0;
             double rv[M0], gp[NT];
 #pragma unroll
@@ -352,6 +359,11 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             const double kfree = isum<NP>(fr ? 1.0 : 0.0);
 #pragma unroll
             for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
+            WBQ_T(t1);
+#ifdef WBQ_STAMPS
+            out.ph[0] += t1 - t0;
+            t0 = t1;
+#endif
             // minimum-norm least squares on the free set: z = A_F^T w (a full-rank Gram by the plain
             // Cholesky, a nearly singular one by the rank-revealing PivChol)
             double wv[M0];
@@ -359,7 +371,16 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
                 PivChol<M0> pc;
                 pc.factor(gp, m0, 1e-12);
                 pc.solve(rv, m0, wv);
+#ifdef WBQ_STAMPS
+                out.ph[6] += 1;
+#endif
             }
+#ifdef WBQ_STAMPS
+            else out.ph[5] += 1;
+            WBQ_T(t1);
+            out.ph[1] += t1 - t0;
+            t0 = t1;
+#endif
             double z = 0.0;
 #pragma unroll
             for (int c = 0; c < M0; ++c) z = fma(acol[c], wv[c], z);
@@ -373,6 +394,11 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             }
             int jb = i;
             iargmin<NP>(al, jb);
+#ifdef WBQ_STAMPS
+            WBQ_T(t1);
+            out.ph[2] += t1 - t0;
+            t0 = t1;
+#endif
             if (inner) {
                 if (!(kfree > 0.0)) {
                     inner = false;
@@ -407,8 +433,13 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
                     if (it >= maxit) inner = false;
                 }
             }
+#ifdef WBQ_STAMPS
+            WBQ_T(t1);
+            out.ph[3] += t1 - t0;
+#endif
         }
         // KKT on the bound variables: w = A0^T (b0 - A0 x)
+        WBQ_T(t0);
         double rf[M0];
 #pragma unroll
         for (int c = 0; c < M0; ++c) rf[c] = acol[c] * xv;
@@ -437,6 +468,10 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
                 freed = best;
             }
         }
+#ifdef WBQ_STAMPS
+        WBQ_T(t1);
+        out.ph[4] += t1 - t0;
+#endif
     }
     out.xv = xv;
     out.st = st;
@@ -758,6 +793,10 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
     } else {
         bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100);
     }
+#ifdef WBQ_STAMPS
+    if (threadIdx.x == 0 && a.stamps)
+        for (int k = 0; k < 8; ++k) a.stamps[blockIdx.x * kStamps + 20 + k] = bv.ph[k];
+#endif
     double xv = bv.xv;
     int st = bv.st, it = bv.it;
     if (bv.capped) out.status = 1;

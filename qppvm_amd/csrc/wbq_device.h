@@ -186,48 +186,130 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
     return (s0 + s1) + (s2 + s3);
 }
 
+// ---------------------------------------------------------------- reductions inside an instance
+// NP = 32: lanes [0, 32) and [32, 64) of the wave are two instances; NP = 64: one. The moves inside a
+// 16-lane row are DPP (quad_perm xor 1, xor 2, row_half_mirror, row_mirror: a VALU operand modifier,
+// ~no latency), the four row partials are then combined from v_readlane (SGPR) values. With
+// __shfl_xor every stage was a pair of ds_bpermute round trips through the LDS unit waited for one by
+// one: a level-0 BVLS step of the config-4 repair (27 sums of 6 x 6 Grams and right-hand sides, the
+// argmin and the KKT max) measured ~20k cycles (scripts/diag_mpc_repair.py). Each stage pairs lanes
+// by an involution and a pair computes a + b and b + a, so every lane of an instance ends with the
+// same bits. Callers run them with every lane of the wave active (values masked, not branched on).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned long long)(unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
+}
+__device__ __forceinline__ double lane_f64(double v, int lane)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | (unsigned long long)lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 template <int NP>
 __device__ __forceinline__ double isum(double v)
 {
-#pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, NP);
-    return v;
+    static_assert(NP == 32 || NP == 64, "isum: NP");
+    v += dpp_f64<kDppXor1>(v);
+    v += dpp_f64<kDppXor2>(v);
+    v += dpp_f64<kDppHalfMirror>(v);
+    v += dpp_f64<kDppMirror>(v);
+    const double r0 = lane_f64(v, 0), r1 = lane_f64(v, 16), r2 = lane_f64(v, 32), r3 = lane_f64(v, 48);
+    if constexpr (NP == 32) return (threadIdx.x & 32) ? r2 + r3 : r0 + r1;
+    else return (r0 + r1) + (r2 + r3);
 }
 
 template <int NP>
 __device__ __forceinline__ double imax(double v)
 {
-#pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, NP));
-    return v;
+    static_assert(NP == 32 || NP == 64, "imax: NP");
+    v = fmax(v, dpp_f64<kDppXor1>(v));
+    v = fmax(v, dpp_f64<kDppXor2>(v));
+    v = fmax(v, dpp_f64<kDppHalfMirror>(v));
+    v = fmax(v, dpp_f64<kDppMirror>(v));
+    const double r0 = lane_f64(v, 0), r1 = lane_f64(v, 16), r2 = lane_f64(v, 32), r3 = lane_f64(v, 48);
+    if constexpr (NP == 32) return (threadIdx.x & 32) ? fmax(r2, r3) : fmax(r0, r1);
+    else return fmax(fmax(r0, r1), fmax(r2, r3));
 }
 
-// (value, index) reductions inside an instance; ties -> lowest index
-template <int NP>
-__device__ __forceinline__ void iargmax(double &v, int &idx)
+// (value, index) reductions inside an instance; ties -> lowest index (a total order, so the tree shape
+// does not change the winner)
+template <bool MAX>
+__device__ __forceinline__ void arg_take(double &v, int &idx, double ov, int oi)
 {
-#pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1) {
-        const double ov = __shfl_xor(v, m, NP);
-        const int oi = __shfl_xor(idx, m, NP);
-        if (ov > v || (ov == v && oi < idx)) {
-            v = ov;
-            idx = oi;
-        }
+    if ((MAX ? ov > v : ov < v) || (ov == v && oi < idx)) {
+        v = ov;
+        idx = oi;
     }
 }
-
-template <int NP>
-__device__ __forceinline__ void iargmin(double &v, int &idx)
+template <int CTRL, bool MAX>
+__device__ __forceinline__ void arg_stage(double &v, int &idx)
 {
+    const double ov = dpp_f64<CTRL>(v);
+    const int oi = dpp_i32<CTRL>(idx);
+    arg_take<MAX>(v, idx, ov, oi);
+}
+template <int NP, bool MAX>
+__device__ __forceinline__ void iarg(double &v, int &idx)
+{
+    static_assert(NP == 32 || NP == 64, "iarg: NP");
+    arg_stage<kDppXor1, MAX>(v, idx);
+    arg_stage<kDppXor2, MAX>(v, idx);
+    arg_stage<kDppHalfMirror, MAX>(v, idx);
+    arg_stage<kDppMirror, MAX>(v, idx);
+    double r[4];
+    int k[4];
 #pragma unroll
-    for (int m = NP / 2; m >= 1; m >>= 1) {
-        const double ov = __shfl_xor(v, m, NP);
-        const int oi = __shfl_xor(idx, m, NP);
-        if (ov < v || (ov == v && oi < idx)) {
-            v = ov;
-            idx = oi;
-        }
+    for (int q = 0; q < 4; ++q) {
+        r[q] = lane_f64(v, 16 * q);
+        k[q] = __builtin_amdgcn_readlane(idx, 16 * q);
+    }
+    arg_take<MAX>(r[0], k[0], r[1], k[1]);
+    arg_take<MAX>(r[2], k[2], r[3], k[3]);
+    if constexpr (NP == 32) {
+        const bool hi = threadIdx.x & 32;
+        v = hi ? r[2] : r[0];
+        idx = hi ? k[2] : k[0];
+    } else {
+        arg_take<MAX>(r[0], k[0], r[2], k[2]);
+        v = r[0];
+        idx = k[0];
+    }
+}
+template <int NP>
+__device__ __forceinline__ void iargmax(double &v, int &idx) { iarg<NP, true>(v, idx); }
+template <int NP>
+__device__ __forceinline__ void iargmin(double &v, int &idx) { iarg<NP, false>(v, idx); }
+
+// K sums at once (the stages of all K interleave)
+template <int NP, int K>
+__device__ __forceinline__ void isum_vec(double (&v)[K])
+{
+    static_assert(NP == 32 || NP == 64, "isum_vec: NP");
+#pragma unroll
+    for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppXor1>(v[c]);
+#pragma unroll
+    for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppXor2>(v[c]);
+#pragma unroll
+    for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppHalfMirror>(v[c]);
+#pragma unroll
+    for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppMirror>(v[c]);
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const double r0 = lane_f64(v[c], 0), r1 = lane_f64(v[c], 16), r2 = lane_f64(v[c], 32), r3 = lane_f64(v[c], 48);
+        if constexpr (NP == 32) v[c] = (threadIdx.x & 32) ? r2 + r3 : r0 + r1;
+        else v[c] = (r0 + r1) + (r2 + r3);
     }
 }
 

