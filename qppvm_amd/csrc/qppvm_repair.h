@@ -85,7 +85,7 @@ struct PivChol {
             if (!stop) {
                 piv[c] = p;
                 k = c + 1;
-                const double lpp = sqrt(best), il = 1.0 / lpp;
+                const double il = frsq(best), lpp = best * il; // (hardware estimate + Newton, ~0.5 ulp)
                 double rp[K];
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
@@ -135,7 +135,7 @@ struct PivChol {
             for (int q = 0; q <= p; ++q) H[tri(p, q)] = p == q ? 1.0 : 0.0;
         double ild[K];
 #pragma unroll
-        for (int c = 0; c < K; ++c) ild[c] = c < k ? 1.0 / Lp[tri(c, c)] : 0.0;
+        for (int c = 0; c < K; ++c) ild[c] = c < k ? frcp(Lp[tri(c, c)]) : 0.0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             bool dep = i < m;
@@ -164,7 +164,7 @@ struct PivChol {
             double dd = H[tri(c, c)];
 #pragma unroll
             for (int j = 0; j < c; ++j) dd = fma(-H[tri(c, j)], H[tri(c, j)], dd);
-            ih[c] = 1.0 / sqrt(dd);
+            ih[c] = frsq(dd);
             H[tri(c, c)] = dd * ih[c];
 #pragma unroll
             for (int r2 = c + 1; r2 < K; ++r2) {
@@ -223,7 +223,7 @@ struct PivChol {
             for (int i = 0; i < K; ++i) v = (piv[c] == i) ? acol[i] : v;
 #pragma unroll
             for (int j = 0; j < c; ++j) v = fma(-Lp[tri(c, j)], q[j], v);
-            q[c] = c < k ? v / Lp[tri(c, c)] : 0.0;
+            q[c] = c < k ? v * frcp(Lp[tri(c, c)]) : 0.0;
         }
     }
 };

@@ -195,6 +195,9 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
 // argmin and the KKT max) measured ~20k cycles (scripts/diag_mpc_repair.py). Each stage pairs lanes
 // by an involution and a pair computes a + b and b + a, so every lane of an instance ends with the
 // same bits. Callers run them with every lane of the wave active (values masked, not branched on).
+// (Measured and not kept: combining the rows with gfx950's v_permlane16/32_swap instead of v_readlane
+// broke every contact-form variant whose dual loop reduces under a lane mask -- the swap moves active
+// lanes only -- while v_readlane reads the row's partial whatever the mask.)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
 {
