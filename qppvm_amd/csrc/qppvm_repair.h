@@ -290,6 +290,101 @@ template <int K>
 constexpr double kCholFastTol = K <= 6 ? 1e-6 : 1e-4;
 
 
+// The BVLS free-set step in the column space, for a free set of at most m0 variables: with A_F (m0 x
+// kfree) of full column rank the minimum-norm least-squares step is z_F = (A_F^T A_F)^-1 A_F^T r, a
+// kfree x kfree SPD solve. The free columns are gathered into slots by ballot + v_readlane (per 32-lane
+// half for NP = 32), every lane factors the small column Gram (unpivoted, static indices) and a free lane
+// takes its slot's component. The row Gram A_F A_F^T of such a step is rank deficient, so the row-space
+// path ran PivChol's select-chain factorisation: ~9.5k of a config-4 repair step's ~18k cycles
+// (scripts/diag_mpc_repair.py). Accepted only when every pivot exceeds tol * (largest diagonal), the
+// regime where PivChol on the row Gram (the same nonzero spectrum) finds full rank kfree and returns the
+// same step; otherwise (dependent free columns) the caller's row path runs. Returns acceptance (the
+// instance's lanes agree); z is this lane's component (free lanes only).
+template <int NP, int M0>
+__device__ __forceinline__ bool bvls_col_step(const double (&acol)[M0], const double (&rv)[M0], bool fr, double tol,
+                                              double &z)
+{
+    const unsigned long long bal = __ballot(fr);
+    const bool upper = NP == 32 && (threadIdx.x & 32);
+    unsigned long long m0m = NP == 32 ? (bal & 0xffffffffull) : bal, m1m = NP == 32 ? (bal >> 32) : 0ull;
+    const int lane = threadIdx.x & (NP - 1);
+    const unsigned long long mine = upper ? m1m : m0m;
+    const int kf = __popcll(mine);
+    const int slot = __popcll(mine & ((1ull << lane) - 1ull));
+    double col[M0][M0]; // [slot][row]
+#pragma unroll
+    for (int q = 0; q < M0; ++q) {
+        const bool v0 = m0m != 0, v1 = m1m != 0;
+        const int l0 = v0 ? (int)__builtin_ctzll(m0m) : 0, l1 = v1 ? (int)__builtin_ctzll(m1m) : 0;
+        m0m &= m0m - 1ull;
+        m1m &= m1m - 1ull;
+#pragma unroll
+        for (int r = 0; r < M0; ++r) {
+            const double a0 = lane_f64(acol[r], l0);
+            double v = v0 ? a0 : 0.0;
+            if constexpr (NP == 32) {
+                const double a1 = lane_f64(acol[r], 32 + l1);
+                v = upper ? (v1 ? a1 : 0.0) : v;
+            }
+            col[q][r] = v;
+        }
+    }
+    double L[M0 * (M0 + 1) / 2], d[M0], il[M0], cmx = 0.0;
+#pragma unroll
+    for (int q = 0; q < M0; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < M0; ++r) v = fma(col[q][r], rv[r], v);
+        d[q] = v;
+#pragma unroll
+        for (int t = 0; t <= q; ++t) {
+            double c = 0.0;
+#pragma unroll
+            for (int r = 0; r < M0; ++r) c = fma(col[q][r], col[t][r], c);
+            L[tri(q, t)] = c;
+        }
+        cmx = fmax(cmx, L[tri(q, q)]);
+    }
+    bool ok = kf > 0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        double dd = c < kf ? L[tri(c, c)] : 1.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) dd = fma(-L[tri(c, k)], L[tri(c, k)], dd);
+        ok = ok && (c >= kf || dd > tol * cmx);
+        const double ic = frsq(fmax(dd, 1e-300));
+        il[c] = ic;
+        L[tri(c, c)] = dd * ic;
+#pragma unroll
+        for (int r = c + 1; r < M0; ++r) {
+            double t = (r < kf && c < kf) ? L[tri(r, c)] : 0.0;
+#pragma unroll
+            for (int k = 0; k < c; ++k) t = fma(-L[tri(r, k)], L[tri(c, k)], t);
+            L[tri(r, c)] = t * ic;
+        }
+    }
+    double y[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        double v = c < kf ? d[c] : 0.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) v = fma(-L[tri(c, k)], y[k], v);
+        y[c] = v * il[c];
+    }
+#pragma unroll
+    for (int c = M0 - 1; c >= 0; --c) {
+        double v = y[c];
+#pragma unroll
+        for (int k = c + 1; k < M0; ++k) v = fma(-L[tri(k, c)], y[k], v);
+        y[c] = v * il[c];
+    }
+    double zz = 0.0;
+#pragma unroll
+    for (int q = 0; q < M0; ++q) zz = (q == slot) ? y[q] : zz;
+    z = zz;
+    return ok && cmx > 0.0;
+}
+
 // BVLS (Stark-Parker; the algorithm of oracle/wbq_oracle.c:wbq_ref_level0) on
 //   min 0.5 ||A z - b||^2  s.t.  lo <= z <= hi
 // with lane i owning variable z_i and its column acol (rows c < m0 of the M0 slots) and every lane
@@ -364,19 +459,33 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             out.ph[0] += t1 - t0;
             t0 = t1;
 #endif
-            // minimum-norm least squares on the free set: z = A_F^T w (a full-rank Gram by the plain
-            // Cholesky, a nearly singular one by the rank-revealing PivChol)
+            // minimum-norm least squares on the free set: at most m0 free variables in the column space
+            // (bvls_col_step); else z = A_F^T w, a full-rank row Gram by the plain Cholesky, a nearly
+            // singular one by the rank-revealing PivChol
+            double zc = 0.0;
+            bool cok = false;
+            if constexpr (M0 <= 6) { // (the 12-row instantiation would hold a 12 x 12 slot matrix)
+                const bool colp = inner && kfree > 0.0 && kfree <= (double)m0;
+                if (__any(colp)) cok = bvls_col_step<NP, M0>(acol, rv, fr, kCholFastTol<M0>, zc) && colp;
+            }
             double wv[M0];
-            if (!chol_solve_full<M0>(gp, m0, rv, wv, kCholFastTol<M0>)) {
-                PivChol<M0> pc;
-                pc.factor(gp, m0, 1e-12);
-                pc.solve(rv, m0, wv);
+#pragma unroll
+            for (int c = 0; c < M0; ++c) wv[c] = 0.0;
+            if (__any(inner && !cok)) {
+                if (!chol_solve_full<M0>(gp, m0, rv, wv, kCholFastTol<M0>)) { // (per instance)
+                    PivChol<M0> pc;
+                    pc.factor(gp, m0, 1e-12);
+                    pc.solve(rv, m0, wv);
 #ifdef WBQ_STAMPS
-                out.ph[6] += 1;
+                    out.ph[6] += cok ? 0 : 1;
+#endif
+                }
+#ifdef WBQ_STAMPS
+                else out.ph[5] += cok ? 0 : 1;
 #endif
             }
 #ifdef WBQ_STAMPS
-            else out.ph[5] += 1;
+            out.ph[7] += cok ? 1 : 0;
             WBQ_T(t1);
             out.ph[1] += t1 - t0;
             t0 = t1;
@@ -384,6 +493,7 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             double z = 0.0;
 #pragma unroll
             for (int c = 0; c < M0; ++c) z = fma(acol[c], wv[c], z);
+            if (cok) z = zc;
             // interpolate back into the box: blocking variable = smallest step fraction < 1
             double al = kInf;
             if (fr) {

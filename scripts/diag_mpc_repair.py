@@ -42,7 +42,7 @@ def main():
     # a block's repair stamps survive until it repairs again: keep each (block, stamps) once
     allr = np.concatenate(rows)
     rep = (allr[:, 12] > allr[:, 8]) & (allr[:, 8] > 0)
-    rr = np.unique(allr[rep][:, list(range(8, 15)) + list(range(20, 27))], axis=0)
+    rr = np.unique(allr[rep][:, list(range(8, 15)) + list(range(20, 28))], axis=0)
     r = rr[:, :7]
     bv = rr[:, 7:].astype(float)  # BVLS split: reductions, solve, z + ratio + argmin, update, outer KKT, fast, pivoted
     ph = np.diff(r[:, :5], axis=1).astype(float)
@@ -55,11 +55,12 @@ def main():
     out["bvls_cycles_fit_const_per_step"] = np.linalg.lstsq(X, ph[:, 1], rcond=None)[0].tolist()
     X = np.stack([np.ones_like(itg), itg], axis=1)
     out["dual_cycles_fit_const_per_step"] = np.linalg.lstsq(X, ph[:, 3], rcond=None)[0].tolist()
-    nit = np.maximum(bv[:, 5] + bv[:, 6], 1.0)
+    nit = np.maximum(bv[:, 5] + bv[:, 6] + bv[:, 7], 1.0)
     out["bvls_split_cycles_per_inner_step"] = {k: float((bv[:, j] / nit).mean()) for j, k in enumerate(
         ["reductions", "solve", "z+ratio+argmin", "update"])}
     out["bvls_outer_kkt_cycles_total_mean"] = float(bv[:, 4].mean())
-    out["bvls_fast_pivoted_solves_mean"] = [float(bv[:, 5].mean()), float(bv[:, 6].mean())]
+    out["bvls_rowfast_pivoted_column_solves_mean"] = [float(bv[:, 5].mean()), float(bv[:, 6].mean()),
+                                                      float(bv[:, 7].mean())]
     out["worst"] = [dict(zip(["gj", "bvls", "pins", "dual"], p.tolist()), bvls_it=int(a), dual_it=int(g))
                     for p, a, g in sorted(zip(ph, itb, itg), key=lambda t: -t[0].sum())[:8]]
     print(json.dumps(out, indent=1))
