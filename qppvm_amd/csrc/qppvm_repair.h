@@ -385,6 +385,95 @@ __device__ __forceinline__ bool bvls_col_step(const double (&acol)[M0], const do
     return ok && cmx > 0.0;
 }
 
+// The same column-space step for the 12-row stacks (two 6-row tasks on level 0, the plugin's own
+// configuration), through the instance's LDS scratch (>= M0 * M0 + NT + M0 doubles, dead during BVLS): a
+// 12 x 12 slot matrix would not fit in registers. Free lanes write their columns into slots, lane e forms
+// entry e of the column Gram (or of A_F^T r) from them, and every lane reads the packed Gram back and
+// factors it as bvls_col_step does. Wave-uniform call (barriers).
+template <int NP, int M0>
+__device__ __forceinline__ bool bvls_col_step_lds(const double (&acol)[M0], const double (&rv)[M0], bool fr, double tol,
+                                                  double &z, double *lds)
+{
+    constexpr int NT = M0 * (M0 + 1) / 2;
+    const unsigned long long bal = __ballot(fr);
+    const bool upper = NP == 32 && (threadIdx.x & 32);
+    const unsigned long long mine = NP == 32 ? (upper ? (bal >> 32) : (bal & 0xffffffffull)) : bal;
+    const int lane = threadIdx.x & (NP - 1);
+    const int kf = __popcll(mine);
+    const int slot = __popcll(mine & ((1ull << lane) - 1ull));
+    double *colm = lds, *ent = lds + M0 * M0;
+    __syncthreads(); // (the region's previous readers are done)
+    if (fr && slot < M0) {
+#pragma unroll
+        for (int r = 0; r < M0; ++r) colm[slot * M0 + r] = acol[r];
+    }
+    __syncthreads();
+    for (int e = lane; e < NT + M0; e += NP) {
+        double v = 0.0;
+        if (e < NT) {
+            int q = 0;
+            while ((q + 1) * (q + 2) / 2 <= e) ++q;
+            const int t = e - q * (q + 1) / 2;
+            if (q < kf && t < kf)
+#pragma unroll
+                for (int r = 0; r < M0; ++r) v = fma(colm[q * M0 + r], colm[t * M0 + r], v);
+        } else {
+            const int q = e - NT;
+            if (q < kf)
+#pragma unroll
+                for (int r = 0; r < M0; ++r) v = fma(colm[q * M0 + r], rv[r], v);
+        }
+        ent[e] = v;
+    }
+    __syncthreads();
+    double L[NT], d[M0], il[M0], cmx = 0.0;
+#pragma unroll
+    for (int e = 0; e < NT; ++e) L[e] = ent[e];
+#pragma unroll
+    for (int q = 0; q < M0; ++q) {
+        d[q] = ent[NT + q];
+        cmx = fmax(cmx, L[tri(q, q)]);
+    }
+    bool ok = kf > 0 && kf <= M0;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        double dd = c < kf ? L[tri(c, c)] : 1.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) dd = fma(-L[tri(c, k)], L[tri(c, k)], dd);
+        ok = ok && (c >= kf || dd > tol * cmx);
+        const double ic = frsq(fmax(dd, 1e-300));
+        il[c] = ic;
+        L[tri(c, c)] = dd * ic;
+#pragma unroll
+        for (int r = c + 1; r < M0; ++r) {
+            double t = (r < kf && c < kf) ? L[tri(r, c)] : 0.0;
+#pragma unroll
+            for (int k = 0; k < c; ++k) t = fma(-L[tri(r, k)], L[tri(c, k)], t);
+            L[tri(r, c)] = t * ic;
+        }
+    }
+    double y[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) {
+        double v = c < kf ? d[c] : 0.0;
+#pragma unroll
+        for (int k = 0; k < c; ++k) v = fma(-L[tri(c, k)], y[k], v);
+        y[c] = v * il[c];
+    }
+#pragma unroll
+    for (int c = M0 - 1; c >= 0; --c) {
+        double v = y[c];
+#pragma unroll
+        for (int k = c + 1; k < M0; ++k) v = fma(-L[tri(k, c)], y[k], v);
+        y[c] = v * il[c];
+    }
+    double zz = 0.0;
+#pragma unroll
+    for (int q = 0; q < M0; ++q) zz = (q == slot) ? y[q] : zz;
+    z = zz;
+    return ok && cmx > 0.0;
+}
+
 // BVLS (Stark-Parker; the algorithm of oracle/wbq_oracle.c:wbq_ref_level0) on
 //   min 0.5 ||A z - b||^2  s.t.  lo <= z <= hi
 // with lane i owning variable z_i and its column acol (rows c < m0 of the M0 slots) and every lane
@@ -407,7 +496,7 @@ struct BvlsOut {
 #endif
 template <int NP, int M0>
 __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (&b0v)[M0], int m0, double lo,
-                                        double hi, bool row, bool active, int st0, int maxit)
+                                        double hi, bool row, bool active, int st0, int maxit, double *lds = nullptr)
 {
     constexpr int NT = M0 * (M0 + 1) / 2;
     const int i = threadIdx.x & (NP - 1); // lane within the instance
@@ -442,15 +531,10 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             if (inner) ++it;
             WBQ_T(t0);
             const bool fr = inner && st == 0;
-            double rv[M0], gp[NT];
+            double rv[M0];
 #pragma unroll
             for (int c = 0; c < M0; ++c) rv[c] = (st == -1 || st == 1) ? acol[c] * xv : 0.0;
-#pragma unroll
-            for (int p = 0; p < M0; ++p)
-#pragma unroll
-                for (int c = 0; c <= p; ++c) gp[tri(p, c)] = fr ? acol[p] * acol[c] : 0.0;
             isum_vec<NP, M0>(rv);
-            isum_vec<NP, NT>(gp);
             const double kfree = isum<NP>(fr ? 1.0 : 0.0);
 #pragma unroll
             for (int c = 0; c < M0; ++c) rv[c] = b0v[c] - rv[c];
@@ -464,14 +548,26 @@ __device__ __forceinline__ BvlsOut bvls(const double (&acol)[M0], const double (
             // singular one by the rank-revealing PivChol
             double zc = 0.0;
             bool cok = false;
-            if constexpr (M0 <= 6) { // (the 12-row instantiation would hold a 12 x 12 slot matrix)
+            {
                 const bool colp = inner && kfree > 0.0 && kfree <= (double)m0;
-                if (__any(colp)) cok = bvls_col_step<NP, M0>(acol, rv, fr, kCholFastTol<M0>, zc) && colp;
+                if constexpr (M0 <= 6) {
+                    if (__any(colp)) cok = bvls_col_step<NP, M0>(acol, rv, fr, kCholFastTol<M0>, zc) && colp;
+                } else { // (a 12 x 12 slot matrix: through LDS)
+                    if (lds && __any(colp))
+                        cok = bvls_col_step_lds<NP, M0>(acol, rv, fr, kCholFastTol<M0>, zc, lds) && colp;
+                }
             }
             double wv[M0];
 #pragma unroll
             for (int c = 0; c < M0; ++c) wv[c] = 0.0;
             if (__any(inner && !cok)) {
+                // the row Gram (only where some instance of the wave needs the row-space step)
+                double gp[NT];
+#pragma unroll
+                for (int p = 0; p < M0; ++p)
+#pragma unroll
+                    for (int c = 0; c <= p; ++c) gp[tri(p, c)] = fr ? acol[p] * acol[c] : 0.0;
+                isum_vec<NP, NT>(gp);
                 if (!chol_solve_full<M0>(gp, m0, rv, wv, kCholFastTol<M0>)) { // (per instance)
                     PivChol<M0> pc;
                     pc.factor(gp, m0, 1e-12);
@@ -901,7 +997,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         }
         bv = bvls<NP, 6>(a6, b6, ml, lo, hi, row, rep, st0, 50 * n + 100);
     } else {
-        bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100);
+        bv = bvls<NP, M0>(acol0, b0v0, ml, lo, hi, row, rep, st0, 50 * n + 100, S + L.QA);
     }
 #ifdef WBQ_STAMPS
     if (threadIdx.x == 0 && a.stamps)
