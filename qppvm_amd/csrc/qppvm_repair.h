@@ -972,7 +972,24 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
         double g = 0.0;
 #pragma unroll
         for (int c = 0; c < M0; ++c) g = fma(acol[c], b0v[c] - rs0[c], g);
-        if (w != 0) st0 = g > 0.0 ? 1 : -1;
+        // two candidate corners: the last sides kept, or every warm variable on the side the gradient at that
+        // corner points to; the start is the one with the smaller level-0 residual. Flipping is what a chattering
+        // plant needs (config 0 stress: the saturated torques swap sides every tick; kept sides there: p50 143 ->
+        // 484 us), keeping what an MPC rollout needs (its bound set drifts; flipped there: up to 86 BVLS steps
+        // against 34, config 4 18.6 vs 23.1 M QP/s; scripts/gpu_r04_p.sh)
+        const int sf = w != 0 ? (g > 0.0 ? 1 : -1) : 0;
+        const double xf = sf < 0 ? lo : (sf > 0 ? hi : xs);
+        double rs1[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) rs1[c] = acol[c] * xf;
+        isum_vec<NP, M0>(rs1);
+        double rk = 0.0, rf = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            rk = fma(b0v[c] - rs0[c], b0v[c] - rs0[c], rk);
+            rf = fma(b0v[c] - rs1[c], b0v[c] - rs1[c], rf);
+        }
+        if (w != 0) st0 = rf < rk ? sf : (w < 0 ? -1 : 1);
     }
     double abm = 0.0;
 #pragma unroll
