@@ -55,11 +55,16 @@ def main():
                "fast_cycles": int(st[5] - st[0])}
         if rep:
             row.update({"gj": int(st[9] - st[8]), "bvls": int(st[10] - st[9]), "pins_eq": int(st[11] - st[10]),
-                        "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14])})
+                        "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14]),
+                        "bvls_split": [int(v) for v in st[20:28]]})
         rows.append(row)
-        print(json.dumps(row), flush=True)
     s.close()
     json.dump(rows, open(out, "w"), indent=1)
+    us = np.array([r["us"] for r in rows])
+    print(json.dumps({"ticks": ticks, "us_p50_p90_p99_max": [float(np.percentile(us, q)) for q in (50, 90, 99, 100)],
+                      "repair_share": float(np.mean([r["repair"] for r in rows]))}))
+    for r in sorted(rows, key=lambda r: -r["us"])[:8]:
+        print(json.dumps(r))
 
 
 if __name__ == "__main__":
