@@ -112,14 +112,27 @@ typedef struct {
     int joint_limits;
     const double *q_min, *q_max; /* [n] joint position limits (ModelInterface::getJointLimits) */
     const double *Kjl, *Djl;     /* [n] barrier stiffness / damping */
-    /* Priority level of each Cartesian task: 0 the first level (its tasks summed), 1 a middle level
-     * between it and the joint task -- the elbow level the reference builds and leaves commented out
-     * of its stack (QPPVMPlugin.cpp:154-166 _elbow_task_left/right, :177-178):
-     *   ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits  = task_level {0, 0, 1, 1}.
-     * The middle level is lexicographic: min ||A1 x - b1||^2 keeping level 0 at its optimum y0*, and
-     * the joint task then keeps both. All zero (a zero-initialised tail): the reference stack.
-     * Needs W1 = I and at most 6 rows per level (else wbq_create returns WBQ_E_UNSUPPORTED). */
+    /* Priority level of each Cartesian task: 0 the first level (its tasks summed), 1 a second
+     * Cartesian level -- the elbow tasks the reference builds on arm1_4 / arm2_4 (QPPVMPlugin.cpp:154-166
+     * _elbow_task_left/right). Level 1 is lexicographic: min ||A1 x - b1||^2 keeping level 0 at its
+     * optimum y0*. At most 6 rows per level (else wbq_create returns WBQ_E_UNSUPPORTED). All zero (a
+     * zero-initialised tail): the reference stack. With no_joint_task = 1 and task_level {0, 0, 1, 1}
+     * this is the reference's commented elbow stack (below); with no_joint_task = 0 the joint task
+     * follows as a third level, ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits: an extension
+     * the reference never spells. Every Cartesian task takes the hands' form A = J M^-1, b = A J^T F
+     * (useInertiaMatrix(true), :139,:151); the reference does not call useInertiaMatrix on the elbow
+     * tasks, and OpenSoT's default form for them is [upstream]: parity unpinned on that point. */
     int task_level[4];
+    /* 1: no joint task -- the stack ends at the last Cartesian level, as in the reference's commented
+     * elbow line, which closes the stack at :178 in place of :179:
+     *   ((ee_r + ee_l) / (elbow_l + elbow_r)) << torque_limits          (QPPVMPlugin.cpp:177-178)
+     * The last level leaves x non-unique (6 rows over n torques); QPOases_sot(.., 1.0) (:188) decides it
+     * by qpOASES' Hessian regularisation eps I, whose eps -> 0 limit is taken here: x = the minimum-norm
+     * point among the lexicographic optima, min ||x||^2 s.t. A0 x = y0*, A1 x = y1*, the box. Solved in
+     * constraint space like W1 = M (joint_weight is ignored); needs m0 + n <= 64. wbq_rollout is
+     * refused (WBQ_E_UNSUPPORTED): its qdd = M^-1 x step is not carried by this path. 0: the joint
+     * task is the last level (the reference's live stack, :179). */
+    int no_joint_task;
 } wbq_desc;
 
 typedef struct {

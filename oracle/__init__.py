@@ -34,7 +34,8 @@ class _Desc(ctypes.Structure):
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
                 ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
                 ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
-                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4)]
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4),
+                ("no_joint_task", ctypes.c_int)]
 
 
 class _Inst(ctypes.Structure):
@@ -90,6 +91,7 @@ def _desc(prob):
     d.select_mode, d.joint_weight = prob.select_mode, prob.joint_weight
     for t, lv in enumerate(getattr(prob, "task_level", None) or ()):
         d.task_level[t] = int(lv)
+    d.no_joint_task = 0 if getattr(prob, "joint_task", True) else 1
     keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
             for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]
     d.Kc, d.Dc, d.Kq, d.Dq, d.tau_max, d.tau_min = [a.ctypes.data for a in keep]

@@ -319,6 +319,13 @@ int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *
         for (int j = 0; j < n; ++j) s += Minv[i * n + j] * timp[j];
         b1[i] = s;
     }
+    if (d->no_joint_task) {
+        /* no joint task (QPPVMPlugin.cpp:177-178 in place of :179): the last level's optima are
+         * decided by qpOASES' eps I regularisation (:188), eps -> 0: min 0.5 ||x||^2 */
+        for (int i = 0; i < n * n; ++i) H1[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < n; ++i) g1[i] = 0.0;
+        goto bounds;
+    }
     /* W1 */
     if (d->joint_weight == WBQ_REF_WEIGHT_INERTIA)
         memcpy(W, in->M, sizeof(double) * n * n);
@@ -347,6 +354,7 @@ int wbq_ref_assemble(const wbq_ref_desc *d, const wbq_ref_instance *in, double *
         for (int k = 0; k < n; ++k) s += tmp[k * n + i] * b1[k];
         g1[i] = -s;
     }
+bounds:
     /* ---- torque limits shifted by -h (QPPVMPlugin.cpp:66-67, 203-205), and with the JointLimits
      * toggle (:169-171) the joint-limit barrier Kjl (q_lim - q) - Djl qd on tau as well */
     for (int j = 0; j < n; ++j) {

@@ -74,10 +74,14 @@ typedef struct {
     int joint_limits;
     const double *q_min, *q_max, *Kjl, *Djl; /* [n] */
     /* priority level of each Cartesian task (include/wbq.h task_level): 0 the first level (the
-     * tasks there summed), 1 a middle level between it and the joint task -- the elbow level of
-     * QPPVMPlugin.cpp:154-166,177-178, ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits.
+     * tasks there summed), 1 a second Cartesian level -- the elbow tasks of QPPVMPlugin.cpp:154-166.
      * All zero: the reference stack. */
     int task_level[WBQ_REF_MAX_TASKS];
+    /* 1: no joint task (include/wbq.h no_joint_task): the stack ends at the last Cartesian level, the
+     * reference's commented elbow stack ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits
+     * (QPPVMPlugin.cpp:177-178 in place of :179); the last level's x is the minimum-norm point among
+     * its optima (H1 = I, g1 = 0: the eps -> 0 limit of QPOases_sot's regularisation, :188). */
+    int no_joint_task;
 } wbq_ref_desc;
 
 /* One instance (all row-major fp64):

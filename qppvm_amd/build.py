@@ -53,33 +53,37 @@ def _stamp(lib: str) -> str:
     return lib + ".srchash"
 
 
+def _flags(diag: bool = False, defines: tuple = ()) -> list:
+    return ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
+            "-I", os.path.join(ROOT, "include"),
+            *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines]]
+
+
 def _stale() -> bool:
-    """The product library is stale when the content hash of its sources differs from the one
-    recorded beside it at link time (no record: fall back to modification times)."""
+    """The product library is stale when the content hash of its compile flags and sources differs
+    from the one recorded beside it at link time (no record: fall back to modification times)."""
     if not os.path.exists(LIB):
         return True
     deps = [os.path.join(CSRC, s) for s in SOURCES] + _headers()
     if os.path.exists(_stamp(LIB)):
         with open(_stamp(LIB)) as f:
-            return f.read().strip() != _digest(_FLAGS_KEY, deps)
+            return f.read().strip() != _digest(_flags(), deps)
     t = os.path.getmtime(LIB)
     return any(os.path.getmtime(p) > t for p in deps)
-
-
-_FLAGS_KEY = ["product", ARCH]
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False, defines: tuple = (),
           out: str | None = None) -> str:
     """diag=True builds libwbq_diag.so with in-kernel phase stamps (never the product);
     defines/out build an experiment variant (scripts/ab_bench.py) at another path."""
+    if defines and out is None:
+        raise ValueError("an experiment build (defines) needs its own output path: the product "
+                         "library and its source stamp describe the product flags only")
     lib = out or (LIB.replace("libwbq.so", "libwbq_diag.so") if diag else LIB)
     if not force and not diag and out is None and not _stale():
         return LIB
-    flags = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-             "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-             "-I", os.path.join(ROOT, "include"),
-             *(["-DWBQ_STAMPS"] if diag else []), *[f"-D{d}" for d in defines]]
+    flags = _flags(diag, defines)
     # one translation unit per process (each holds its own kernels), then one link. An object is
     # keyed by the content hash of its flags, its source and every header, so it is reused only
     # when none of them changed (WBQ_INCREMENTAL=1 reuses objects on a forced build too)
@@ -87,7 +91,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     os.makedirs(objdir, exist_ok=True)
     hdrs = _headers()
     # the record is taken before compiling: an edit made while the build runs leaves it stale
-    record = _digest(_FLAGS_KEY, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
+    record = _digest(flags, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
     objs = [os.path.join(objdir, os.path.splitext(s)[0] + "_" +
                          _digest(flags, [os.path.join(CSRC, s)] + _headers(os.path.join(CSRC, s))) + ".o")
             for s in SOURCES]
@@ -107,7 +111,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
         os.replace(c[-1], c[-1][:-4])
     subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", *objs, "-o", lib + ".tmp"])
     os.replace(lib + ".tmp", lib)
-    if lib == LIB and not defines:
+    if lib == LIB:
         with open(_stamp(LIB), "w") as f:
             f.write(record + "\n")
     return lib

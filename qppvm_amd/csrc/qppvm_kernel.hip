@@ -1080,11 +1080,14 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {
-    if (a.joint_weight == 1) return launch_qppvm_w1m(a, stream, mid);
+    if (a.joint_weight == 1 || a.minnorm) return launch_qppvm_w1m(a, stream, mid);
     // (a middle level, m_l0 < m0, takes the 12-row instantiation: its repair carries the middle step)
+    // (both branches: the 6-row instantiation compiles the middle level out, so a split stack of
+    // at most 6 rows in total would be solved as one summed level there)
+    const bool six = a.m0 <= 6 && a.m_l0 >= a.m0;
     if (a.n <= 32)
-        return (a.m0 <= 6 && a.m_l0 >= a.m0) ? launch_np<32, 6>(a, stream, mid) : launch_np<32, kM0Max>(a, stream, mid);
-    return a.m0 <= 6 ? launch_np<64, 6>(a, stream, mid) : launch_np<64, kM0Max>(a, stream, mid);
+        return six ? launch_np<32, 6>(a, stream, mid) : launch_np<32, kM0Max>(a, stream, mid);
+    return six ? launch_np<64, 6>(a, stream, mid) : launch_np<64, kM0Max>(a, stream, mid);
 }
 
 }  // namespace wbq

@@ -16,6 +16,16 @@
 // inside the loop): level 0 is not attainable at b0, and the repair kernel computes y* and
 // the pinned limits by BVLS (the level0_repair of the W1 = I path) and solves again.
 //
+// The stack without a joint task (a.minnorm, wbq_desc no_joint_task: the reference's commented
+// elbow stack ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits, QPPVMPlugin.cpp:177-178) runs the
+// same loop with H = I -- the eps -> 0 limit of QPOases_sot's regularisation (:188) decides the
+// last level's optima by min 0.5 ||x||^2:
+//   rows A = [G M^-1 ; I],  H^-1 A^T = A^T = [M^-1 G^T, I],  Gamma = [G M^-2 G^T, G M^-1 ; M^-1 G^T, I],
+//   x0 = 0,  x = (M^-1 G^T) lam_E + lam_B.
+// Every Cartesian row (level 0 and a second level, task_level) enters as an equality at its
+// target; the repair computes y0*, y1* and the pins of both levels (level0_repair) when some
+// target is not attainable.
+//
 // One instance per wave64 block, lane i <-> joint i for the staging and the Gauss-Jordan,
 // lane ci <-> constraint row ci for the active set (m0 + n <= 64).
 #include "wbq_kernels.h"
@@ -63,7 +73,7 @@ struct W1mLayout {
             o += tt > ov ? tt : ov;
         }
         XV = o; o += 64;           // x
-        X0 = o; o += 64;           // x0 = tau_imp
+        X0 = o; o += 64;           // x0 = tau_imp (0 without a joint task)
         U0 = o; o += 64;           // u_imp = M^-1 tau_imp
         VV = o; o += 72;
         LV = o; o += 72;
@@ -138,6 +148,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     constexpr int NRC = 1 + M0; // Gauss-Jordan right-hand sides: tau_imp, G^T
     const int T = a.ntasks, n = a.n, m0 = a.m0;
     const W1mLayout L(n, T, m0, NQ, NRC);
+    const bool mn = a.minnorm; // H = I, x0 = 0: no joint task (wbq_desc no_joint_task)
     const bool row = i < n;
     const int ic = row ? i : n - 1;
 
@@ -190,10 +201,10 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         if (it * 64 + i < T * 24) S[L.PS + it * 64 + i] = pv[it];
 #pragma unroll
     for (int r = 0; r < NQ; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
-    if (row) { // Gamma bound row m0 + i: [G^T row i | M row i]
+    if (row) { // Gamma bound row m0 + i: [G^T row i | M row i]  (without a joint task: [X row i | e_i])
 #pragma unroll
         for (int r = 0; r < NQ; ++r)
-            if (r < n) S[L.GM + (m0 + i) * L.GS + m0 + r] = A[r];
+            if (r < n) S[L.GM + (m0 + i) * L.GS + m0 + r] = mn ? (r == i ? 1.0 : 0.0) : A[r];
     }
     __syncthreads();
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
@@ -211,7 +222,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     double gc[M0];
 #pragma unroll
     for (int c = 0; c < M0; ++c) gc[c] = (c < m0 && i < NQ) ? S[L.JR + a.row_sel[c < m0 ? c : 0] * NQ + i] : 0.0;
-    if (row) {
+    if (row && !mn) {
 #pragma unroll
         for (int c = 0; c < M0; ++c)
             if (c < m0) {
@@ -243,13 +254,22 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         for (int c = 0; c < M0; ++c)
             if (c < m0) S[L.XG + c * L.QS + i] = rhs[1 + c];
     }
+    if (row && mn) { // both off-diagonal Gamma blocks: (G M^-1)_c j = X_j c
+#pragma unroll
+        for (int c = 0; c < M0; ++c)
+            if (c < m0) {
+                S[L.GM + (m0 + i) * L.GS + c] = rhs[1 + c];
+                S[L.GM + c * L.GS + m0 + i] = rhs[1 + c];
+            }
+    }
     S[L.U0 + i] = (i < NQ && row) ? rhs[0] : 0.0;
-    S[L.X0 + i] = tau_imp_i;
-    S[L.XV + i] = tau_imp_i;
+    S[L.X0 + i] = mn ? 0.0 : tau_imp_i;
+    S[L.XV + i] = mn ? 0.0 : tau_imp_i;
     __syncthreads();
 
     // ---------------------- 3. level-0 rows: Gamma_EE, targets b0, activities at x0
-    // b0_c = G_c M^-1 J_t^T F_t = X_c . (J_t^T F_t), s0_c = X_c . tau_imp (lane c < m0)
+    // b0_c = G_c M^-1 J_t^T F_t = X_c . (J_t^T F_t), s0_c = X_c . x0 (lane c < m0);
+    // Gamma_EE row i = X_i . Gamma[c][m0 + :] = G M^-1 G^T (W1 = M) or X^T X (no joint task)
     double b0 = 0.0, s0 = 0.0;
     if (i < m0) {
         const double *xg = S + L.XG + i * L.QS;
@@ -396,7 +416,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     if (imax<64>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
     if (status != 0) tau_i = h_i; // "SOLVER ERROR!" fallback: tau_qp = 0 (:246-249)
     if (row) a.tau[b * n + i] = tau_i;
-    if (a.integrate) { // qdd = M^-1 x = u_imp + (M^-1 G^T) lam_E + lam_B
+    if (a.integrate && !mn) { // qdd = M^-1 x = u_imp + (M^-1 G^T) lam_E + lam_B (refused without a joint task)
         S[L.RV + i] = i < gs.k ? gs.sgn * gs.lam : 0.0;
         S[L.AC + i] = (double)gs.act;
         __syncthreads();
@@ -518,14 +538,16 @@ hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t m
     if (a.B <= 0) return hipSuccess;
     // TM = 2 when at most two tasks: 12 J-row loads per lane instead of 24 (the stage stays under
     // the 63 outstanding vector loads, as the W1 = I fast kernel)
+    // (a second Cartesian level takes the 12-row instantiation: its repair carries the middle step)
+    const bool six = a.m0 <= 6 && a.m_l0 >= a.m0;
     if (a.ntasks <= 2) {
         if (a.n <= 32)
-            return a.m0 <= 6 ? launch_w1m_t<32, 6, 2>(a, stream, mid) : launch_w1m_t<32, kM0Max, 2>(a, stream, mid);
-        return a.m0 <= 6 ? launch_w1m_t<64, 6, 2>(a, stream, mid) : launch_w1m_t<64, kM0Max, 2>(a, stream, mid);
+            return six ? launch_w1m_t<32, 6, 2>(a, stream, mid) : launch_w1m_t<32, kM0Max, 2>(a, stream, mid);
+        return six ? launch_w1m_t<64, 6, 2>(a, stream, mid) : launch_w1m_t<64, kM0Max, 2>(a, stream, mid);
     }
     if (a.n <= 32)
-        return a.m0 <= 6 ? launch_w1m_t<32, 6, kTMax>(a, stream, mid) : launch_w1m_t<32, kM0Max, kTMax>(a, stream, mid);
-    return a.m0 <= 6 ? launch_w1m_t<64, 6, kTMax>(a, stream, mid) : launch_w1m_t<64, kM0Max, kTMax>(a, stream, mid);
+        return six ? launch_w1m_t<32, 6, kTMax>(a, stream, mid) : launch_w1m_t<32, kM0Max, kTMax>(a, stream, mid);
+    return six ? launch_w1m_t<64, 6, kTMax>(a, stream, mid) : launch_w1m_t<64, kM0Max, kTMax>(a, stream, mid);
 }
 
 }  // namespace wbq

@@ -310,12 +310,14 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
                 sel[m0++] = t * 6 + r;
             }
     }
-    // W1 = M runs the active set in constraint space, one lane per level-0 row and torque limit
-    if (d.joint_weight == WBQ_WEIGHT_INERTIA && m0 + d.n > 64) return WBQ_E_UNSUPPORTED;
-    // a middle level: at least one task on level 0, W1 = I (the u-space repair carries the middle
-    // step), at most 6 rows per level (the repair's 6-row bvls_eq blocks)
-    if (mid && (m_l0 == 0 || d.joint_weight != WBQ_WEIGHT_IDENTITY || m_l0 > 6 || m0 - m_l0 > 6))
-        return WBQ_E_UNSUPPORTED;
+    if (d.no_joint_task != 0 && d.no_joint_task != 1) return WBQ_E_INVALID;
+    // W1 = M and the stack without a joint task run the active set in constraint space, one lane per
+    // Cartesian row and torque limit
+    const bool cspace = d.joint_weight == WBQ_WEIGHT_INERTIA || d.no_joint_task;
+    if (cspace && m0 + d.n > 64) return WBQ_E_UNSUPPORTED;
+    // a second Cartesian level: at least one task on level 0, at most 6 rows per level (the
+    // repair's 6-row bvls_eq blocks)
+    if (mid && (m_l0 == 0 || m_l0 > 6 || m0 - m_l0 > 6)) return WBQ_E_UNSUPPORTED;
     wbq_ctx *c = new wbq_ctx();
     c->d = d;
     c->d.Kc = c->d.Dc = c->d.Kq = c->d.Dq = c->d.tau_max = c->d.tau_min = nullptr;
@@ -365,7 +367,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
     if (!ok) return cleanup(WBQ_E_DEVICE);
     {
         // scratch lanes per instance (the W1 = M repair runs one instance per wave)
-        const size_t np = d.joint_weight == WBQ_WEIGHT_INERTIA ? 64 : (size_t)wbq::lanes_per_instance(d.n);
+        const size_t np = cspace ? 64 : (size_t)wbq::lanes_per_instance(d.n);
         ok = hipMalloc(&c->u_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
@@ -589,6 +591,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.m_l0 = c->m_l0;
     a.select_mode = c->d.select_mode;
     a.joint_weight = c->d.joint_weight;
+    a.minnorm = c->d.no_joint_task;
     a.max_iter = c->d.max_iter;
     a.limits_crossed = c->limits_crossed;
     for (int t = 0; t < wbq::kTMax; ++t) a.row_mask[t] = t < c->d.ntasks ? c->d.row_mask[t] : 0;
@@ -691,6 +694,8 @@ int wbq_rollout(wbq_ctx *c, int steps, double dt)
 {
     if (!c) return WBQ_E_INVALID;
     if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout: steps >= 0, dt >= 0");
+    if (c->form == WBQ_FORM_QPPVM && c->d.no_joint_task)
+        return fail(c, WBQ_E_UNSUPPORTED, "wbq_rollout: not with no_joint_task (qdd = M^-1 x is not carried)");
     // QPPVM W1 = I with n <= 32 and m0 <= 6: the whole rollout in one launch (qppvm_rollout_kernel);
     // WBQ_OPT_FUSED_ROLLOUT = 0 keeps one launch per step (the A/B of the two)
     if (c->opt_fused && steps > 0 && c->form == WBQ_FORM_QPPVM && c->d.joint_weight == WBQ_WEIGHT_IDENTITY &&
@@ -712,6 +717,8 @@ int wbq_rollout_rbd(wbq_ctx *c, wbq_rbd_ctx *rbd, int steps, double dt)
         return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: model n / tasks / device differ from the context's "
                                       "(contact form: the waist and the nc contact frames)");
     if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout_rbd: steps >= 0, dt >= 0");
+    if (c->form == WBQ_FORM_QPPVM && c->d.no_joint_task)
+        return fail(c, WBQ_E_UNSUPPORTED, "wbq_rollout_rbd: not with no_joint_task (qdd = M^-1 x is not carried)");
     WBQ_HIP(hipSetDevice(c->device));
     if (c->in_pending && c->in_stream != c->stream) {
         WBQ_HIP(hipStreamWaitEvent(c->stream, c->in_copied, 0));

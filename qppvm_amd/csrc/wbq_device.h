@@ -198,6 +198,22 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
 // (Measured and not kept: combining the rows with gfx950's v_permlane16/32_swap instead of v_readlane
 // broke every contact-form variant whose dual loop reduces under a lane mask -- the swap moves active
 // lanes only -- while v_readlane reads the row's partial whatever the mask.)
+// The reductions read the four row partials with v_readlane whatever EXEC holds: a call under a lane
+// mask would read stale partials of inactive lanes. Diagnostic builds (-DWBQ_STAMPS) check the
+// precondition at every reduction and report a violation (printf from the first active lane; no
+// trap: a fault can take the whole GPU down); the product build does not.
+#ifdef WBQ_STAMPS
+#define WBQ_FULL_EXEC()                                                                 \
+    do {                                                                                \
+        const unsigned long long ex_ = __builtin_amdgcn_read_exec();                    \
+        if (ex_ != ~0ull && (int)(threadIdx.x & 63) == __builtin_ctzll(ex_))             \
+            printf("wbq: reduction under a lane mask (exec %llx) in block %d at %s:%d\n", \
+                   ex_, (int)blockIdx.x, __FILE__, __LINE__);                            \
+    } while (0)
+#else
+#define WBQ_FULL_EXEC() do {} while (0)
+#endif
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
 {
@@ -224,6 +240,7 @@ template <int NP>
 __device__ __forceinline__ double isum(double v)
 {
     static_assert(NP == 32 || NP == 64, "isum: NP");
+    WBQ_FULL_EXEC();
     v += dpp_f64<kDppXor1>(v);
     v += dpp_f64<kDppXor2>(v);
     v += dpp_f64<kDppHalfMirror>(v);
@@ -237,6 +254,7 @@ template <int NP>
 __device__ __forceinline__ double imax(double v)
 {
     static_assert(NP == 32 || NP == 64, "imax: NP");
+    WBQ_FULL_EXEC();
     v = fmax(v, dpp_f64<kDppXor1>(v));
     v = fmax(v, dpp_f64<kDppXor2>(v));
     v = fmax(v, dpp_f64<kDppHalfMirror>(v));
@@ -267,6 +285,7 @@ template <int NP, bool MAX>
 __device__ __forceinline__ void iarg(double &v, int &idx)
 {
     static_assert(NP == 32 || NP == 64, "iarg: NP");
+    WBQ_FULL_EXEC();
     arg_stage<kDppXor1, MAX>(v, idx);
     arg_stage<kDppXor2, MAX>(v, idx);
     arg_stage<kDppHalfMirror, MAX>(v, idx);
@@ -300,6 +319,7 @@ template <int NP, int K>
 __device__ __forceinline__ void isum_vec(double (&v)[K])
 {
     static_assert(NP == 32 || NP == 64, "isum_vec: NP");
+    WBQ_FULL_EXEC();
 #pragma unroll
     for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppXor1>(v[c]);
 #pragma unroll

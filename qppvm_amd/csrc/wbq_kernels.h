@@ -49,6 +49,8 @@ struct QppvmArgs {
     int m_l0;        // of them level 0's (the first m_l0); the rest a middle level (wbq_desc task_level)
     int select_mode; // WBQ_SELECT_*
     int joint_weight; // WBQ_WEIGHT_*: W1 = I (qppvm_kernel.hip) or W1 = M (qppvm_w1m_kernel.hip)
+    int minnorm;     // no joint task (wbq_desc no_joint_task): the last level's min-norm x, in the
+                     // constraint-space kernel (qppvm_w1m_kernel.hip) with H = I
     int max_iter;    // active-set step cap
     int limits_crossed; // some tau_min > tau_max (batch-shared limits): every instance infeasible
     int row_mask[kTMax];

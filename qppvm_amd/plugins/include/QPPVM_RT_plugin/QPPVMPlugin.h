@@ -40,10 +40,16 @@ public:
     // the JointLimits constraint the reference builds and comments out of its stack (:169-173):
     // set before init_control_plugin
     void set_joint_limits(bool on) { _use_joint_limits = on; }
-    // the elbow tasks the reference builds (:154-166, on arm1_4 / arm2_4) and leaves commented out of
-    // its stack (:177-178), as a middle level: ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits.
+    // the elbow tasks the reference builds (:154-166, on arm1_4 / arm2_4) and the stack its commented
+    // line :178 closes in place of :179: ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits, no joint task
+    // (include/wbq.h no_joint_task). with_joint_task = true keeps the joint task as a third level,
+    // ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits: an extension the reference never spells.
     // Set before init_control_plugin
-    void set_elbow_level(bool on) { _use_elbow = on; }
+    void set_elbow_level(bool on, bool with_joint_task = false)
+    {
+        _use_elbow = on;
+        _elbow_joint = with_joint_task;
+    }
     int ntasks() const { return (int)_ee_links.size(); }
     const Eigen::VectorXd &joint_limit(int which) const { return which ? _q_max : _q_min; }
     const Eigen::VectorXd &joint_limit_gain(int which) const { return which ? _d_jl : _k_jl; }
@@ -65,6 +71,7 @@ private:
     // elbow level the elbow tasks follow (:154-166: left, then right, as in :178's sum)
     std::vector<std::string> _ee_links{"arm2_7", "arm1_7"};
     bool _use_elbow = false;
+    bool _elbow_joint = false;
     double _start_time = 0.0;
     int _status = 0;
     int _iters = 0;

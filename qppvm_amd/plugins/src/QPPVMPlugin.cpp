@@ -79,6 +79,9 @@ bool QPPVMPlugin::init_control_plugin(XBot::Handle::Ptr handle) // :42-199
         d.row_mask[t] = 0x7;                  // OpenSoT::Indices::range(0,2) (:134, :147, :158, :165)
         d.task_level[t] = t < 2 ? 0 : 1;      // the elbows below the hands (:177-178)
     }
+    // the elbow stack as the reference's commented line closes it (:177-178 in place of :179): no
+    // joint task, unless the three-level extension was asked for
+    d.no_joint_task = (_use_elbow && !_elbow_joint) ? 1 : 0;
     d.select_mode = WBQ_SELECT_SUBTASK;
     d.joint_weight = WBQ_WEIGHT_IDENTITY;
     d.max_batch = 1;

@@ -98,7 +98,7 @@ int main(int argc, char **argv)
 {
     int ticks = 10000, dump_ticks = 0, n = -1;
     const char *dump = nullptr;
-    bool forceacc = false, stress = false, set_ref = false, joint_limits = false, elbow = false;
+    bool forceacc = false, stress = false, set_ref = false, joint_limits = false, elbow = false, elbow_joint = false;
     int wd = 3;
     double mu = 0.0;
     const char *log_prefix = nullptr;
@@ -109,7 +109,8 @@ int main(int argc, char **argv)
         else if (!std::strcmp(argv[k], "--stress")) stress = true;
         else if (!std::strcmp(argv[k], "--set-ref")) set_ref = true; // QPPVMPlugin.cpp:217-223
         else if (!std::strcmp(argv[k], "--joint-limits")) joint_limits = true; // :169-171
-        else if (!std::strcmp(argv[k], "--elbow")) elbow = true;               // :154-166, :177-178
+        else if (!std::strcmp(argv[k], "--elbow")) elbow = true;               // :154-166, :177-178 (no joint task)
+        else if (!std::strcmp(argv[k], "--elbow-joint")) elbow = elbow_joint = true; // the 3-level extension
         else if (!std::strcmp(argv[k], "--wrench6")) wd = 6;                   // ForceAcc.cpp:67
         else if (!std::strcmp(argv[k], "--mu") && k + 1 < argc) mu = std::atof(argv[++k]);
         else if (!std::strcmp(argv[k], "--log") && k + 1 < argc) log_prefix = argv[++k];
@@ -132,7 +133,7 @@ int main(int argc, char **argv)
     if (log_prefix) plugin.set_log_prefix(log_prefix);
     plugin.set_reference_trajectory(set_ref);
     plugin.set_joint_limits(joint_limits);
-    plugin.set_elbow_level(elbow);
+    plugin.set_elbow_level(elbow, elbow_joint);
     if (!plugin.init_control_plugin(handle)) {
         std::fprintf(stderr, "init_control_plugin failed\n");
         return 2;

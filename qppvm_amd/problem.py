@@ -72,10 +72,13 @@ class QPPVMProblem:
     q_max: np.ndarray | float = np.pi
     Kjl: np.ndarray | float = 50.0
     Djl: np.ndarray | float = 20.0
-    # priority level per Cartesian task: 0 = the first level (summed), 1 = a middle level between it
-    # and the joint task -- the elbow level QPPVMPlugin.cpp:154-166,177-178 leaves commented out,
-    # ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits (include/wbq.h task_level). None: all 0.
+    # priority level per Cartesian task: 0 = the first level (summed), 1 = a second Cartesian level --
+    # the elbow tasks of QPPVMPlugin.cpp:154-166 (include/wbq.h task_level). None: all 0.
     task_level: tuple | None = None
+    # False: no joint task -- the stack ends at the last Cartesian level, the reference's commented
+    # elbow stack ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits (QPPVMPlugin.cpp:177-178 in place of
+    # :179), x the minimum-norm point among that level's optima (include/wbq.h no_joint_task)
+    joint_task: bool = True
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -104,6 +107,7 @@ class QPPVMProblem:
         self.tau_max = _vec(self.tau_max, n, "tau_max")
         self.tau_min = -self.tau_max if self.tau_min is None else _vec(self.tau_min, n, "tau_min")
         self.joint_limits = bool(self.joint_limits)
+        self.joint_task = bool(self.joint_task)
         for k in ("q_min", "q_max", "Kjl", "Djl"):
             setattr(self, k, _vec(getattr(self, k), n, k))
         if self.select_mode not in (SELECT_SUBTASK, SELECT_TASK):

@@ -42,7 +42,8 @@ class Desc(ctypes.Structure):
                 ("Kc", ctypes.c_void_p), ("Dc", ctypes.c_void_p), ("Kq", ctypes.c_void_p),
                 ("Dq", ctypes.c_void_p), ("tau_max", ctypes.c_void_p), ("tau_min", ctypes.c_void_p),
                 ("joint_limits", ctypes.c_int), ("q_min", ctypes.c_void_p), ("q_max", ctypes.c_void_p),
-                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4)]
+                ("Kjl", ctypes.c_void_p), ("Djl", ctypes.c_void_p), ("task_level", ctypes.c_int * 4),
+                ("no_joint_task", ctypes.c_int)]
 
 
 class Inputs(ctypes.Structure):
@@ -164,6 +165,7 @@ class QPPVMSolver:
         d.select_mode, d.joint_weight = prob.select_mode, prob.joint_weight
         for t, lv in enumerate(prob.task_level):
             d.task_level[t] = int(lv)
+        d.no_joint_task = 0 if prob.joint_task else 1
         d.max_batch, d.max_iter = self.max_batch, int(prob.max_iter)
         self._keep = [np.ascontiguousarray(getattr(prob, k), dtype=np.float64)
                       for k in ("Kc", "Dc", "Kq", "Dq", "tau_max", "tau_min")]

@@ -62,17 +62,19 @@ def load_golden_contact(n, fname=None):
         yield g, prob, inp, {"tau": z[pre + "tau"], "x": z[pre + "x"]}
 
 
-def load_golden_elbow():
-    """Yield (group, QPPVMProblem, inputs, expected) of the three-level stack fixtures
-    (tests/golden/qppvm_elbow.npz, make_golden_elbow.py): task_level (0, 0, 1, 1), the elbow level of
-    QPPVMPlugin.cpp:154-166,177-178."""
+def load_golden_elbow(literal=False):
+    """Yield (group, QPPVMProblem, inputs, expected) of the elbow-stack fixtures (make_golden_elbow.py):
+    task_level (0, 0, 1, 1) with the elbow tasks of QPPVMPlugin.cpp:154-166. literal: the reference's
+    commented stack ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits, no joint task (:177-178 in place
+    of :179; tests/golden/qppvm_elbow_literal.npz); else the three-level extension with the joint task
+    (tests/golden/qppvm_elbow.npz)."""
     from qppvm_amd.problem import QPPVMProblem
-    z = np.load(os.path.join(GOLDEN, "qppvm_elbow.npz"))
+    z = np.load(os.path.join(GOLDEN, "qppvm_elbow_literal.npz" if literal else "qppvm_elbow.npz"))
     for g in z["groups"]:
         g = str(g)
         pre = g + "__"
         prob = QPPVMProblem(n=int(z[pre + "n"]), ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1),
-                            tau_max=z[pre + "tau_max"])
+                            tau_max=z[pre + "tau_max"], joint_task=not literal)
         inp = {k: np.ascontiguousarray(z[pre + k]) for k in INPUT_KEYS}
         exp = {k: z[pre + k] for k in ("tau", "y", "kat") if pre + k in z}
         yield g, prob, inp, exp

@@ -96,9 +96,10 @@ def _null(E, k):
     return Vt[r:].T
 
 
-def level1_np(H, g, Aeq, beq, lb, ub, x0, maxit=500):
+def level1_np(H, g, Aeq, beq, lb, ub, x0, maxit=500, gscale=None):
     """Monotone primal active set (Nocedal & Wright alg. 16.3, null-space EQP) from the
-    feasible level-0 point; accepted only with a KKT certificate."""
+    feasible level-0 point; accepted only with a KKT certificate. gscale: the gradient scale of
+    the tolerances (default max(1, |g|); a problem with g = 0 passes the scale of H x)."""
     n = H.shape[0]
     x = np.clip(x0.copy(), lb, ub)
     lo = x <= lb
@@ -119,10 +120,11 @@ def level1_np(H, g, Aeq, beq, lb, ub, x0, maxit=500):
                 np.zeros(Aeq.shape[0])
             lam = gr + Aeq.T @ nu  # lambda_lo - lambda_hi on the bound variables
             wrong = np.where(lo & (lb < ub), -lam, np.where(hi, lam, -np.inf))
-            tol_g = 1e-9 * max(1.0, np.abs(g).max(), np.abs(Aeq.T @ nu).max())
+            gs = max(1.0, np.abs(g).max()) if gscale is None else gscale
+            tol_g = 1e-9 * max(gs, np.abs(Aeq.T @ nu).max())
             if wrong.max() <= tol_g:
                 # certificate: stationarity on F, feasibility, signs (checked above)
-                assert np.abs(lam[F]).max(initial=0.0) <= 1e-8 * max(1.0, np.abs(g).max())
+                assert np.abs(lam[F]).max(initial=0.0) <= 1e-8 * gs
                 assert np.abs(Aeq @ x - beq).max() <= 1e-8 * max(1.0, np.abs(beq).max())
                 assert np.all(x >= lb) and np.all(x <= ub)
                 return x

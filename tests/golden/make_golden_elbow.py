@@ -1,9 +1,13 @@
-"""Generate the golden fixtures of the three-level QPPVM stack (run in the build container).
+"""Generate the golden fixtures of the QPPVM stacks with the elbow level (run in the build container).
 
-The elbow level the reference builds and leaves commented out of its stack
-(QPPVMPlugin.cpp:154-166 _elbow_task_left/right, :177-178):
+The elbow tasks the reference builds (QPPVMPlugin.cpp:154-166 _elbow_task_left/right) and the stack
+its commented line :178 closes in place of :179:
+    ((ee_r + ee_l) / (elbow_l + elbow_r)) << torque_limits          (no joint task; --literal)
+i.e. task_level (0, 0, 1, 1) over four Cartesian impedance tasks and no_joint_task = 1 (include/wbq.h):
+the last level's x is the minimum-norm point among its optima (the eps -> 0 limit of QPOases_sot's
+regularisation, :188), min ||x||^2 over {A0 x = y0*, A1 x = y1*, box}. And the three-level extension
+that keeps the joint task after the elbows:
     ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << torque_limits
-i.e. task_level (0, 0, 1, 1) over four Cartesian impedance tasks (include/wbq.h wbq_desc.task_level).
 An *independent* numpy/scipy restatement that shares no code with oracle/wbq_oracle.c or the HIP
 kernels, built on the two-level generator (make_golden.py: its assembly, level-0 BVLS and level-1
 active set):
@@ -12,12 +16,15 @@ active set):
 * the middle level min ||A1 x - b1||^2 s.t. A0 x = y0*, box (level-0 pins fixed): a monotone primal
   active set whose equality-constrained steps are null-space least squares (pinv), accepted only with
   a KKT certificate (stationarity modulo the equality rows, multiplier signs) -> y1*;
-* the joint task over {A0 x = y0*, A1 x = y1*, box, pins} by make_golden.level1_np;
-* bounds-inactive groups carry the closed form KAT-1 with the stacked 12-row G (every level
-  attained), which the lexicographic answer must equal.
+* the last level over {A0 x = y0*, A1 x = y1*, box, pins} by make_golden.level1_np: the joint task
+  (H1, g1), or without it min 0.5 ||x||^2 (H = I, g = 0);
+* bounds-inactive groups carry a closed form with the stacked 12-row A = G M^-1 (every level
+  attained), which the lexicographic answer must equal: KAT-1 with the joint task, the
+  pseudo-inverse x = A^T (A A^T)^-1 b without it.
 
-Output: tests/golden/qppvm_elbow.npz (groups per n in {14, 30, 39}).
-Usage: python tests/golden/make_golden_elbow.py
+Output: tests/golden/qppvm_elbow.npz (three levels) or, with --literal, tests/golden/
+qppvm_elbow_literal.npz (no joint task); groups per n in {14, 30, 39}.
+Usage: python tests/golden/make_golden_elbow.py [--literal]
 """
 from __future__ import annotations
 
@@ -85,6 +92,8 @@ def level_mid_np(A1, b1, E, e, lb, ub, x0, maxit=2000):
 
 
 def solve3_np(prob, inp, b):
+    """The elbow stack: level 0, the elbow level, then the joint task (prob.joint_task) or the
+    minimum-norm x."""
     a = assemble_np(prob, inp, b)  # rows in task order: tasks 0, 1 (level 0), then 2, 3 (level 1)
     ml = prob.m_l0
     A0, b0, A1, b1 = a["A0"][:ml], a["b0"][:ml], a["A0"][ml:], a["b0"][ml:]
@@ -105,7 +114,11 @@ def solve3_np(prob, inp, b):
     lb2[up] = ub2[up]
     ub2[dn] = lb2[dn]
     Aeq, beq = np.vstack([A0, A1]), np.concatenate([y0, y1])
-    x = level1_np(a["H1"], a["g1"], Aeq, beq, lb2, ub2, np.clip(x1, lb2, ub2))
+    if prob.joint_task:
+        x = level1_np(a["H1"], a["g1"], Aeq, beq, lb2, ub2, np.clip(x1, lb2, ub2))
+    else:  # min 0.5 ||x||^2: the gradient is x itself
+        gs = max(1.0, np.abs(a["lb"]).max(), np.abs(a["ub"]).max(), np.abs(x1).max())
+        x = level1_np(np.eye(prob.n), np.zeros(prob.n), Aeq, beq, lb2, ub2, np.clip(x1, lb2, ub2), gscale=gs)
     return x + inp["h"][b], beq, a
 
 
@@ -118,23 +131,30 @@ GROUPS = [
 ]
 
 
-def make(n, seed):
+def kat_minnorm(inp, b, a):
+    """Bounds inactive, every level attained, no joint task: the minimum-norm solution of the 12
+    stacked rows A x = b (A = G M^-1, the pseudo-inverse)."""
+    A, y = a["A0"], a["b0"]
+    return A.T @ np.linalg.solve(A @ A.T, y) + inp["h"][b]
+
+
+def make(n, seed, joint=True):
     out = {}
     for gi, (name, count, q) in enumerate(GROUPS):
-        probe = QPPVMProblem(n=n, tau_max=1e6, **TASKS)
+        probe = QPPVMProblem(n=n, tau_max=1e6, joint_task=joint, **TASKS)
         inp = qppvm_instances(probe, count, seed=seed * 100 + gi)
         if q is None:
             prob = probe
         else:
             t0 = np.concatenate([solve3_np(probe, inp, b)[0] for b in range(count)])
-            prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(t0), q)), **TASKS)
+            prob = QPPVMProblem(n=n, tau_max=float(np.quantile(np.abs(t0), q)), joint_task=joint, **TASKS)
         taus, ys, kats = [], [], []
         for b in range(count):
             tau, y, a = solve3_np(prob, inp, b)
             taus.append(tau)
             ys.append(y)
             if q is None:
-                k = kat(prob, inp, b, a)  # the stacked 12 rows all attained
+                k = kat(prob, inp, b, a) if joint else kat_minnorm(inp, b, a)  # the 12 rows all attained
                 assert np.abs(k - tau).max() <= 1e-8 * max(1, np.abs(k).max()), name
                 kats.append(k)
             act = np.mean((tau - inp["h"][b] <= a["lb"] + 1e-9) | (tau - inp["h"][b] >= a["ub"] - 1e-9))
@@ -152,13 +172,15 @@ def make(n, seed):
 
 
 def main():
+    literal = "--literal" in sys.argv
     data, groups = {}, []
-    for n, seed in ((14, 11), (30, 12), (39, 13)):
-        d = make(n, seed)
+    seeds = ((14, 21), (30, 22), (39, 23)) if literal else ((14, 11), (30, 12), (39, 13))
+    for n, seed in seeds:
+        d = make(n, seed, joint=not literal)
         data.update(d)
         groups += [f"n{n}_{g[0]}" for g in GROUPS]
     data["groups"] = np.array(groups)
-    path = os.path.join(HERE, "qppvm_elbow.npz")
+    path = os.path.join(HERE, "qppvm_elbow_literal.npz" if literal else "qppvm_elbow.npz")
     np.savez_compressed(path, **data)
     print("wrote", path, os.path.getsize(path), "bytes")
 

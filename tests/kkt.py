@@ -61,7 +61,12 @@ def qppvm_certificate(oracle, prob, inp, b, tau):
         E = Al if E is None else np.concatenate([E, Al], axis=0)
     G = A0 @ M
     timp = _tau_imp(prob, inp, b)
-    r = np.linalg.solve(M, x - timp) if prob.joint_weight == 0 else x - timp
+    # M times the last level's gradient: W1 = I M^-1 (x - tau_imp), W1 = M x - tau_imp, and without
+    # the joint task (min 0.5 ||x||^2, the reference's commented elbow stack) M x
+    if not getattr(prob, "joint_task", True):
+        r = M @ x
+    else:
+        r = np.linalg.solve(M, x - timp) if prob.joint_weight == 0 else x - timp
     act = np.where(~free)[0]
     K = np.concatenate([G.T, M[:, act]], axis=1)
     lam, *_ = np.linalg.lstsq(K, r, rcond=None)

@@ -100,3 +100,24 @@ def test_three_level_certificate_accepts_oracle(oracle_lib, n, q):
         assert differ.sum() >= 4
         bad = [kkt.qppvm_certificate(oracle_lib, p3, inp, b, t2[b])["level0"] for b in np.where(differ)[0]]
         assert max(bad) > 1e-6
+
+
+def test_certificate_elbow_literal(oracle_lib):
+    """The lexicographic certificate of the reference's commented elbow stack (no joint task: the last
+    level's gradient is x itself, QPPVMPlugin.cpp:177-178): the oracle's outputs pass on every
+    fixture group, and the three-level stack's torques (joint task kept) fail its stationarity where
+    the two differ."""
+    import kkt
+    from conftest import load_golden_elbow
+    fails = 0
+    for g, prob, inp, exp in load_golden_elbow(True):
+        tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
+        joint = QPPVMProblem(n=prob.n, ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1), tau_max=prob.tau_max)
+        tj, _, _ = oracle_lib.qppvm_batch(joint, inp)
+        for b in range(tau.shape[0]):
+            c = kkt.qppvm_certificate(oracle_lib, prob, inp, b, tau[b])
+            assert max(c["primal"], c["level0"], c["stat"], c["sign"]) <= 1e-9, (g, b, c)
+            if np.abs(tj[b] - tau[b]).max() > 1e-6 * np.abs(tau[b]).max():
+                cj = kkt.qppvm_certificate(oracle_lib, prob, inp, b, tj[b])
+                fails += max(cj["stat"], cj["sign"]) > 1e-6
+    assert fails >= 10

@@ -79,13 +79,16 @@ def test_infeasible_bounds_fallback(oracle_lib):
     np.testing.assert_array_equal(tau, inp["h"])
 
 
-def test_oracle_three_level_golden(oracle_lib):
-    """The oracle's lexicographic three-level chain (task_level: the elbow level between the hands and
-    the joint task, QPPVMPlugin.cpp:154-166,177-178) against the independent numpy/scipy fixtures
-    (tests/golden/make_golden_elbow.py), including the groups where the elbow level is not attained."""
+@pytest.mark.parametrize("literal", [True, False])
+def test_oracle_elbow_stacks(oracle_lib, literal):
+    """The oracle's lexicographic elbow stacks against the independent numpy/scipy fixtures
+    (tests/golden/make_golden_elbow.py), including the groups where the elbow level is not attained:
+    the reference's commented stack ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits with no joint task
+    and the minimum-norm x (QPPVMPlugin.cpp:177-178 in place of :179; closed form: the pseudo-inverse
+    of the 12 stacked rows), and the three-level extension with the joint task (KAT-1)."""
     from conftest import load_golden_elbow, rel_err
     seen_unattained = 0
-    for g, prob, inp, exp in load_golden_elbow():
+    for g, prob, inp, exp in load_golden_elbow(literal):
         tau, st, _ = oracle_lib.qppvm_batch(prob, inp)
         assert (st == 0).all(), g
         assert rel_err(tau, exp["tau"]) <= 1e-8, (g, rel_err(tau, exp["tau"]))
@@ -95,3 +98,30 @@ def test_oracle_three_level_golden(oracle_lib):
             a = oracle_lib.assemble(prob, inp, b)
             seen_unattained += np.abs(exp["y"][b][6:] - a["b0"][6:]).max() > 1e-6 * max(1, np.abs(a["b0"]).max())
     assert seen_unattained >= 4  # the middle level binds in the fixtures
+
+
+def test_oracle_elbow_literal_minnorm(oracle_lib):
+    """Without the joint task the stack's x is the minimum-norm point of the last level's optima: any
+    feasible move along the null space of the 12 rows that keeps the box raises ||x|| (checked on the
+    bounds-inactive groups by perturbation), and the joint-task stack gives other torques."""
+    from conftest import load_golden_elbow, rel_err
+    rng = np.random.default_rng(3)
+    for g, prob, inp, exp in load_golden_elbow(True):
+        if "kat" not in exp:
+            continue
+        tau, _, _ = oracle_lib.qppvm_batch(prob, inp)
+        for b in range(tau.shape[0]):
+            a = oracle_lib.assemble(prob, inp, b)
+            x = tau[b] - inp["h"][b]
+            _, S, Vt = np.linalg.svd(a["A0"])
+            Z = Vt[int((S > 1e-12 * S[0]).sum()):].T
+            # x lies in the row space of the 12 rows (orthogonal to every feasible direction)
+            assert np.abs(Z.T @ x).max() <= 1e-9 * np.linalg.norm(x), g
+            for _ in range(8):
+                d = Z @ rng.normal(size=Z.shape[1])
+                d *= 1e-3 * np.linalg.norm(x) / np.linalg.norm(d)
+                assert np.linalg.norm(x + d) > np.linalg.norm(x)
+        joint = type(prob)(**{**{k: getattr(prob, k) for k in ("n", "ntasks", "row_mask", "task_level")},
+                              "tau_max": prob.tau_max, "joint_task": True})
+        tj, _, _ = oracle_lib.qppvm_batch(joint, inp)
+        assert rel_err(tj, tau) > 1e-6, g

@@ -221,26 +221,37 @@ def test_forceacc_matlogger(tmp_path):
 
 def test_dummy_driver_elbow_level(tmp_path, oracle_lib):
     """The elbow toggle of the QPPVM shell: the elbow tasks the reference builds on arm1_4 / arm2_4
-    (QPPVMPlugin.cpp:154-166) as the middle level its commented stack line puts them on (:177-178),
-    ((ee_r + ee_l) / (elbow_l + elbow_r)) / joint << limits. Every dumped tick re-solved by the
-    oracle's three-level chain; the nominal and the stress plant (level-0 repairs on every tick)."""
+    (QPPVMPlugin.cpp:154-166) in the stack its commented line :178 closes in place of :179,
+    ((ee_r + ee_l) / (elbow_l + elbow_r)) << limits -- no joint task, the last level's x the
+    minimum-norm optimum (`--elbow`); and the three-level extension with the joint task kept
+    (`--elbow-joint`). Every dumped tick re-solved by the oracle's chain; the nominal and the stress
+    plant (level-0 repairs on every tick)."""
     from qppvm_amd import build
     driver = build.build_plugins()[1]
-    for stress in (False, True):
-        dump = str(tmp_path / f"dump_elbow{int(stress)}.bin")
-        r = subprocess.run([driver, "--ticks", "200", "--dump", dump, "40", "--elbow"] + (["--stress"] if stress else []),
-                           capture_output=True, text=True, timeout=240)
-        assert r.returncode == 0, r.stderr[-2000:]
-        n, d = read_dump(dump)
-        assert d["J"].shape[1] == 4
-        prob = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1))
-        inp = {k: np.ascontiguousarray(d[k]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
-        tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
-        np.testing.assert_array_equal(d["status"], st_r)
-        ok = st_r == 0
-        assert ok.sum() >= len(ok) - 2
-        assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, (stress, rel_err(d["tau"][ok], tau_r[ok]))
-        if stress:  # the elbow level changes the torques against the reference's two-level stack
-            two = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7))
-            tau_2, _, _ = oracle_lib.qppvm_batch(two, inp)
-            assert rel_err(tau_2, d["tau"]) > 1e-6
+    for flag, joint in (("--elbow", False), ("--elbow-joint", True)):
+        for stress in (False, True):
+            dump = str(tmp_path / f"dump_elbow{int(joint)}{int(stress)}.bin")
+            r = subprocess.run([driver, "--ticks", "200", "--dump", dump, "40", flag] + (["--stress"] if stress else []),
+                               capture_output=True, text=True, timeout=240)
+            assert r.returncode == 0, r.stderr[-2000:]
+            n, d = read_dump(dump)
+            assert d["J"].shape[1] == 4
+            prob = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1),
+                                joint_task=joint)
+            inp = {k: np.ascontiguousarray(d[k]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
+            tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+            np.testing.assert_array_equal(d["status"], st_r)
+            ok = st_r == 0
+            assert ok.sum() >= len(ok) - 2
+            assert rel_err(d["tau"][ok], tau_r[ok]) <= TOL, (flag, stress, rel_err(d["tau"][ok], tau_r[ok]))
+            if not stress:  # the other elbow stack gives other torques (the joint task moves x off the
+                # min-norm point; on the stress plant every torque saturates at the level-0 repair's
+                # unique point, where the two stacks agree)
+                other = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7), task_level=(0, 0, 1, 1),
+                                     joint_task=not joint)
+                tau_o, _, _ = oracle_lib.qppvm_batch(other, inp)
+                assert rel_err(tau_o, d["tau"]) > 1e-6
+            if stress:  # the elbow level changes the torques against the reference's two-level stack
+                two = QPPVMProblem(n=n, tau_max=150.0, ntasks=4, row_mask=(7, 7, 7, 7))
+                tau_2, _, _ = oracle_lib.qppvm_batch(two, inp)
+                assert rel_err(tau_2, d["tau"]) > 1e-6
