@@ -41,6 +41,7 @@
 #include "dual_gi.h"
 #include "qppvm_repair.h"
 #include "fric_lsi.h"
+#include "qr_gi.h"
 
 #include <type_traits>
 
@@ -278,6 +279,60 @@ struct ContactGi {
         }
         if (i >= n) dx *= ieps;
         S[L->XV + i] = (pass == 0 ? (i < n ? S[L->X0 + i] : 0.0) : S[L->XV + i]) + dx;
+    }
+};
+
+// The contact problem for the QR-form fallback (qr_gi.h): row normals a_ci = [A_q row; force
+// coefficients] and H^-1 a_ci = [X^T slot ci; force coefficients / eps_f] (the same data the
+// constraint-space loop reads), activities through the ContactGi rows.
+template <int NQ, bool TR, int NFM, bool FR>
+struct ContactQr {
+    const ContactGi<NQ, TR, NFM, FR> *gi;
+    double *S;
+    const ContactLayout *L;
+    int n, nf, i, nx, dim, m;
+    double ieps;
+    __device__ double own_activity() const { return gi->activity(i); }
+    __device__ double own_norm2() const
+    {
+        double q2 = 0.0;
+        if constexpr (TR) {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) q2 = fma(gi->aq[j], gi->aq[j], q2);
+        } else {
+            const double *rq = row_q(S, *L, i);
+            if (rq)
+                for (int j = 0; j < n; ++j) q2 = fma(rq[j], rq[j], q2);
+        }
+        for (int f = 0; f < nf; ++f) {
+            const double c = fcoef<FR>(S, *L, i, f);
+            q2 = fma(c, c, q2);
+        }
+        return q2;
+    }
+    __device__ void normal(int p, double sg, double *ap, double *hp) const
+    {
+        const bool qb = p < L->NJ + 6; // a joint or waist row: it has an acceleration part
+        if constexpr (TR) { // the acceleration part lives in row p's own lane (registers)
+            if (i == p) {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j < n) ap[j] = qb ? sg * gi->aq[j] : 0.0;
+            }
+        } else if (i < n) {
+            const double *rq = row_q(S, *L, p);
+            ap[i] = rq ? sg * rq[i] : 0.0;
+        }
+        if (i < n) hp[i] = qb ? sg * S[L->XT + p * L->QS + i] : 0.0;
+        if (i >= n && i < nx) {
+            const double c = sg * fcoef<FR>(S, *L, p, i - n);
+            ap[i] = c;
+            hp[i] = c * ieps;
+        }
+        if (i >= nx) {
+            ap[i] = 0.0;
+            hp[i] = 0.0;
+        }
     }
 };
 
@@ -723,6 +778,8 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ, FR>(a, b, S, L, i, h_i, lo, hi, l0cap, wkeep);
         __syncthreads();
     }
+    const double lo_rep = lo, hi_rep = hi; // the pinned level 1 (the QR fallback's problem)
+    const int wkeep_rep = wkeep;
 
     // ------------------------------------ 6. dual active set in constraint space
     // Slot a (lane a < k) = a-th active row: act (compact row), sgn (normal = sgn * a_act),
@@ -871,7 +928,30 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     if (gs.status != 1 && gs.status != 3) break;
     }
     int status = gs.status;
-    const int iters = gs.iters + it0;
+    int iters = gs.iters + it0;
+    if constexpr (REPAIR) {
+        // The constraint-space loop failed on the pinned level 1 (and on the retry without the pins):
+        // near a degenerate vertex its Gamma complements cannot tell dependent rows from independent
+        // ones. The QR-form loop (qr_gi.h) solves the same pinned problem from x0 with an
+        // explicit basis of the active normals. Its LDS follows the layout (a.qr_fallback: it fits).
+        if (status != 0 && a.qr_fallback && !notspd && !a.limits_crossed && !l0cap) {
+            const int kp = (ci >= NJ && ci < NJ + 6 && !((wkeep_rep >> (ci - NJ)) & 1)) ? 0 : kind_free;
+            if (i < L.NX) S[L.XV + i] = i < n ? S[L.X0 + i] : 0.0;
+            __syncthreads();
+            const int dim = n + WD * __popc((unsigned)cm & ((1u << nc) - 1u));
+            ContactGi<NQ, TR, NFM, FR> gi{S, &L, n, nf, i, ieps, dim};
+            if constexpr (TR) {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) gi.aq[j] = aq[j];
+            }
+            const ContactQr<NQ, TR, NFM, FR> pq{&gi, S, &L, n, nf, i, L.NX, dim, ME, ieps};
+            const QrGiLayout Q(L.NX, L.NX);
+            int itq = 0;
+            status = qr_gi(pq, S + L.XV, S + L.SIZE, Q, L.NX, i, kp, lo_rep, hi_rep, 10 * (L.NX + ME) + 50, itq);
+            iters += itq;
+            __syncthreads();
+        }
+    }
     if constexpr (!REPAIR) {
         // no step exists: the waist task is not attainable at b_w (the rows are boxes in
         // (tau_a, f), so nothing else can be infeasible) -- the repair kernel solves level 0 first.
@@ -966,9 +1046,13 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
     // the register slot vectors hold every active row
     if (!TR && KMR > 0 && (L.ME > KMR || a.nc * WD > KMR - 12)) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
+    // the repair kernel's LDS also holds the QR-form fallback's basis when it fits the CU's 160 KB
+    const size_t lds_qr = lds + sizeof(double) * QrGiLayout(L.NX, L.NX).SIZE;
+    const bool qr = lds_qr <= 160 * 1024;
+    const size_t lds2 = qr ? lds_qr : lds;
     if (a.prepare) {
         const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR, WD>, lds);
-        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR, WD>, lds);
+        return e != hipSuccess ? e : ensure_dynamic_lds((const void *)contact_repair_kernel<NQ, TR, KMR, WD>, lds2);
     }
     hipLaunchKernelGGL((contact_kernel<NQ, TR, KMR, WD>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     hipError_t e2 = hipGetLastError();
@@ -978,7 +1062,9 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
         if (e2 != hipSuccess) return e2;
     }
     const unsigned grid = follow_blocks(a.fg.est[1], 1, kContactRepairGrid, a.B);
-    hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR, WD>), dim3(grid), dim3(64), lds, stream, a);
+    ContactArgs a2 = a;
+    a2.qr_fallback = qr ? 1 : 0;
+    hipLaunchKernelGGL((contact_repair_kernel<NQ, TR, KMR, WD>), dim3(grid), dim3(64), lds2, stream, a2);
     return hipGetLastError();
 }
 

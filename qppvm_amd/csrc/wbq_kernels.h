@@ -177,6 +177,8 @@ struct ContactArgs {
     // warm start: the side (+1 lower / -1 upper, 0 inactive) of every constraint row in the last
     // solve's final active set, per instance ([B][64]; dual_gi.h warm_extend)
     signed char *ws_rows;
+    // set by the launcher for the repair kernel: its LDS holds the QR-form fallback (qr_gi.h)
+    int qr_fallback;
 };
 
 // Semi-implicit Euler of one joint of instance b in place (lane i owns joint i of its

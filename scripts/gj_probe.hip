@@ -159,6 +159,149 @@ __device__ __forceinline__ bool block_gj2(double (&A)[NC], double (&rhs)[NR], in
     return notspd;
 }
 
+// block_gj with the trailing update's panel reads issued a chunk ahead (the compiler's own schedule kept
+// one ds_read_b128 in flight and waited for each: the elimination ran at the LDS latency, not at its
+// bandwidth or the FP64 rate). CH columns per chunk, two chunks in registers. UNI: one update form for
+// every row (hh = D^-1 e_ri - e_ri inside the pivot block), no cc * A multiply per column.
+template <int NP, int NR, int RHS, int NC, int CH, bool UNI>
+__device__ __forceinline__ bool block_gj3(double (&A)[NC], double (&rhs)[NR], int n, int i, double *PN, double *RH)
+{
+    static_assert(NC % kGjBS == 0 && NC <= NP, "block_gj3: NC");
+    constexpr int BS = kGjBS;
+    bool notspd = false;
+    if (i < NP) {
+#pragma unroll
+        for (int c = 0; c < BS; ++c) PN[i * BS + c] = A[c];
+    }
+    if (i < BS) {
+#pragma unroll
+        for (int m = 0; m < NR; ++m) RH[i * RHS + m] = rhs[m];
+    }
+#pragma unroll
+    for (int kb = 0; kb < NC / BS; ++kb) {
+        const int k = kb * BS;
+        if (k < n) {
+            __syncthreads();
+            const double *pn = PN + (kb & 1) * NP * BS;
+            const double *rh = RH + (kb & 1) * BS * RHS;
+            double *pnn = PN + ((kb + 1) & 1) * NP * BS;
+            double *rhn = RH + ((kb + 1) & 1) * BS * RHS;
+            // the lookahead panel and the first trailing chunk are read with the pivot block
+            double la[BS][BS];
+#pragma unroll
+            for (int u = 0; u < BS; ++u)
+#pragma unroll
+                for (int c = 0; c < BS; ++c) la[u][c] = (k + BS + u < NC) ? pn[(k + BS + u) * BS + c] : 0.0;
+            constexpr int J0 = 0; (void)J0;
+            double d[BS][BS];
+#pragma unroll
+            for (int r = 0; r < BS; ++r)
+#pragma unroll
+                for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
+            double rv[BS][NR];
+#pragma unroll
+            for (int c = 0; c < BS; ++c)
+#pragma unroll
+                for (int m = 0; m < NR; ++m) rv[c][m] = rh[c * RHS + m];
+            double il[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double dd = d[c][c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
+                notspd |= !(dd > 0.0);
+                il[c] = frsq(dd);
+#pragma unroll
+                for (int r = c + 1; r < BS; ++r) {
+                    double t = d[r][c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
+                    d[r][c] = t * il[c];
+                }
+            }
+            const int ri = i - k;
+            const bool inK = ri >= 0 && ri < BS;
+            double y[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                double v = inK ? (ri == c ? 1.0 : 0.0) : A[k + c];
+#pragma unroll
+                for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
+                y[c] = v * il[c];
+            }
+#pragma unroll
+            for (int c = BS - 1; c >= 0; --c) {
+                double v = y[c];
+#pragma unroll
+                for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
+                y[c] = v * il[c];
+            }
+            const double cc = inK ? 0.0 : 1.0;
+            double hh[BS];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) hh[c] = UNI ? (inK ? y[c] - (ri == c ? 1.0 : 0.0) : -y[c]) : (inK ? y[c] : -y[c]);
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                double v = UNI ? rhs[m] : cc * rhs[m];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], rv[c][m], v);
+                rhs[m] = v;
+            }
+#pragma unroll
+            for (int u = 0; u < BS; ++u) {
+                const int j = k + BS + u;
+                if (j < NC) {
+                    double v = UNI ? A[j] : cc * A[j];
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) v = fma(hh[c], la[u][c], v);
+                    A[j] = v;
+                }
+            }
+            if (k + BS < n) {
+                if (i < NP) {
+#pragma unroll
+                    for (int c = 0; c < BS; ++c)
+                        if (k + BS + c < NC) pnn[i * BS + c] = A[(k + BS + c) < NC ? k + BS + c : NC - 1];
+                }
+                const int rn = i - (k + BS);
+                if (rn >= 0 && rn < BS) {
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) rhn[rn * RHS + m] = rhs[m];
+                }
+            }
+            // trailing columns in chunks of CH, the next chunk's reads issued before this chunk's FMAs
+            constexpr int NCH = (NC + CH - 1) / CH;
+            double pv[2][CH][BS];
+#pragma unroll
+            for (int ch = 0; ch <= NCH; ++ch) {
+                const int j0 = k + 2 * BS + ch * CH;
+                if (ch < NCH && j0 < NC) {
+#pragma unroll
+                    for (int u = 0; u < CH; ++u)
+#pragma unroll
+                        for (int c = 0; c < BS; ++c) pv[ch & 1][u][c] = (j0 + u < NC) ? pn[(j0 + u) * BS + c] : 0.0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const int jp = j0 - CH;
+                if (ch > 0 && jp < NC) {
+#pragma unroll
+                    for (int u = 0; u < CH; ++u) {
+                        const int j = jp + u;
+                        if (j < NC) {
+                            double v = UNI ? A[j] : cc * A[j];
+#pragma unroll
+                            for (int c = 0; c < BS; ++c) v = fma(hh[c], pv[(ch - 1) & 1][u][c], v);
+                            A[j] = v;
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    return notspd;
+}
+
 // LDS per instance: G rows [M0][NP], panels [NB][NP][BS] (left) or [2][NP][BS] (right), RHS [2][BS][8]
 constexpr int kG = 0, kPN = M0 * NP, kPNsize = NB * NP * BS, kRH = kPN + kPNsize, kSIZE = kRH + 2 * BS * 8;
 
@@ -224,7 +367,10 @@ __global__ __launch_bounds__(64, 2) void gj_kernel(const Args a)
 #endif
         __syncthreads();
         NOSTAMP(1);
-        if constexpr (MODE >= 5) (void)block_gj2<NP, NR, 8, NC>(A, rhs, N, i, S + kPN, S + kRH);
+        if constexpr (MODE == 7) (void)block_gj3<NP, NR, 8, NC, 4, false>(A, rhs, N, i, S + kPN, S + kRH);
+        else if constexpr (MODE == 8) (void)block_gj3<NP, NR, 8, NC, 4, true>(A, rhs, N, i, S + kPN, S + kRH);
+        else if constexpr (MODE == 9) (void)block_gj3<NP, NR, 8, NC, 8, false>(A, rhs, N, i, S + kPN, S + kRH);
+        else if constexpr (MODE >= 5) (void)block_gj2<NP, NR, 8, NC>(A, rhs, N, i, S + kPN, S + kRH);
         else (void)block_gj<NP, NR, 8, NC>(A, rhs, N, i, S + kPN, S + kRH);
         NOSTAMP(10);
     } else {
@@ -365,7 +511,7 @@ int main(int argc, char **argv)
     }
     for (auto &v : G) v = nd(rng);
     for (auto &v : R) v = nd(rng);
-    double *dM, *dG, *dR, *dX[3], *dY[2];
+    double *dM, *dG, *dR, *dX[6], *dY[2];
     unsigned long long *dst;
     CHECK(hipMalloc(&dst, sizeof(unsigned long long) * 16 * (B / 2)));
     CHECK(hipMemset(dst, 0, sizeof(unsigned long long) * 16 * (B / 2)));
@@ -375,7 +521,7 @@ int main(int argc, char **argv)
     CHECK(hipMalloc(&dM, M.size() * 8));
     CHECK(hipMalloc(&dG, G.size() * 8));
     CHECK(hipMalloc(&dR, R.size() * 8));
-    CHECK(hipMalloc(&dX[2], R.size() * 8));
+    for (int v = 2; v < 6; ++v) CHECK(hipMalloc(&dX[v], R.size() * 8));
     for (int v = 0; v < 2; ++v) {
         CHECK(hipMalloc(&dX[v], R.size() * 8));
         CHECK(hipMalloc(&dY[v], G.size() * 8));
@@ -389,16 +535,19 @@ int main(int argc, char **argv)
     CHECK(hipFuncSetAttribute((const void *)gj_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     CHECK(hipFuncSetAttribute((const void *)gj_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     CHECK(hipFuncSetAttribute((const void *)gj_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CHECK(hipFuncSetAttribute((const void *)gj_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CHECK(hipFuncSetAttribute((const void *)gj_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CHECK(hipFuncSetAttribute((const void *)gj_kernel<7>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     CHECK(hipFuncSetAttribute((const void *)gj_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     CHECK(hipFuncSetAttribute((const void *)gj_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const char *names[7] = {"right", "left", "right-synthetic-M", "left-synthetic-M", "stage-only", "inv-block",
-                            "inv-block-synthetic-M"};
+    const char *names[10] = {"right", "left", "right-synthetic-M", "left-synthetic-M", "stage-only", "inv-block",
+                             "inv-block-synthetic-M", "chunk4", "chunk4-uni", "chunk8"};
     for (int round = 0; round < 2; ++round)
-        for (int v = 0; v < 7; ++v) {
-            Args a{dM, dG, dR, dX[v == 5 ? 2 : (v & 1)], dY[v & 1], dst, dsel, B};
+        for (int v = 0; v < 10; ++v) {
+            Args a{dM, dG, dR, dX[v == 5 ? 2 : (v >= 7 ? v - 4 : (v & 1))], dY[v & 1], dst, dsel, B};
             auto launch = [&]() {
                 switch (v) {
                 case 0: hipLaunchKernelGGL(gj_kernel<0>, dim3(B / 2), dim3(64), lds, 0, a); break;
@@ -407,6 +556,9 @@ int main(int argc, char **argv)
                 case 3: hipLaunchKernelGGL(gj_kernel<3>, dim3(B / 2), dim3(64), lds, 0, a); break;
                 case 5: hipLaunchKernelGGL(gj_kernel<5>, dim3(B / 2), dim3(64), lds, 0, a); break;
                 case 6: hipLaunchKernelGGL(gj_kernel<6>, dim3(B / 2), dim3(64), lds, 0, a); break;
+                case 7: hipLaunchKernelGGL(gj_kernel<7>, dim3(B / 2), dim3(64), lds, 0, a); break;
+                case 8: hipLaunchKernelGGL(gj_kernel<8>, dim3(B / 2), dim3(64), lds, 0, a); break;
+                case 9: hipLaunchKernelGGL(gj_kernel<9>, dim3(B / 2), dim3(64), lds, 0, a); break;
                 default: hipLaunchKernelGGL(gj_kernel<4>, dim3(B / 2), dim3(64), lds, 0, a); break;
                 }
             };
@@ -485,6 +637,12 @@ int main(int argc, char **argv)
                 r2 = std::fmax(r2, std::fabs(s));
             }
         std::printf("inv-block: max |X - X_right| %.3e (max |X| %.3e), residual %.3e\n", d2, xm, r2);
+        for (int v = 3; v < 6; ++v) {
+            CHECK(hipMemcpy(X2.data(), dX[v], X2.size() * 8, hipMemcpyDeviceToHost));
+            double dv = 0;
+            for (size_t k = 0; k < X0.size(); ++k) dv = std::fmax(dv, std::fabs(X0[k] - X2[k]));
+            std::printf("%s: max |X - X_right| %.3e\n", names[v + 4], dv);
+        }
     }
     return 0;
 }

@@ -74,29 +74,23 @@ def test_contact_ext_config1_identical(wbq_mod, oracle_lib):
     assert np.abs(tau - tau[0]).max() == 0.0
 
 
-FRICTION_MAX_MISS = 8
-
-
 @pytest.mark.parametrize("mu", [0.3, 0.5])
 def test_contact_level0_repair_friction(wbq_mod, oracle_lib, mu):
     """Level 0 not attainable with the friction pyramid on (the reference's stack
     waist / (postural + feet), ForceAcc.cpp:131-137, keeps the waist at its level-0 optimum under
-    every constraint): the GPU solves level 0 over the box AND the pyramid faces (fric_lsi.h, an LSI
-    in the BVLS pattern) as the oracle's level-0 QP does (oracle/wbq_oracle_contact.c:413-447), and
-    level 1 holds the faces and box sides its multipliers pin. The test_contact_level0_repair sweep
-    (n = 12, nc = 4, torque rows at the 40 % quantile, 20 seeds, 1,280 instances) with the cone on:
-    every instance the oracle solves, the GPU solves with the oracle's tau (MAX_MISS = 0); where the
-    oracle fails, a GPU solution carries the level-1 KKT certificate (1e-9) and the level-0 LSI
-    certificate at 1e-8: those are the degenerate instances (the oracle's own dual loop ends
-    numerically there), where the final point's waist value carries the level-0 step's roundoff
-    (observed 2e-9). Until round 4 the GPU gave up with status 2 whenever the box-only level-0 point
-    violated a face.
-
-    FRICTION_MAX_MISS instances per mu may end with a failure status (tau = h, never a wrong tau)
-    where the oracle solves: 2 of 1,251 at mu = 0.3 and 6 of 1,253 at mu = 0.5 on MI355X (round 4),
-    the main or the level-1 dual loop reaching an active set on which a violated torque or friction row
-    is dependent to roundoff (scripts/emulate_dual_gi.py replays them: its Schur complement ~1e-7
-    against Gamma_pp ~1e8, the force block's 1 / eps_f scale) -- DESIGN.md 5."""
+    every constraint and returns false only when infeasible, :189-193): the GPU solves level 0 over the
+    box AND the pyramid faces (fric_lsi.h, an LSI in the BVLS pattern) as the oracle's level-0 QP does
+    (oracle/wbq_oracle_contact.c:413-447), and level 1 holds the faces and box sides its multipliers
+    pin. The test_contact_level0_repair sweep (n = 12, nc = 4, torque rows at the 40 % quantile, 20
+    seeds, 1,280 instances) with the cone on: every instance the oracle solves, the GPU solves with the
+    oracle's tau (no miss allowed). Near a degenerate vertex the constraint-space dual loop cannot tell
+    a dependent row from an independent one (its Schur complements in Gamma carry the 1 / eps_f force
+    scale's roundoff); there the repair kernel finishes level 1 with the QR-form loop
+    (qppvm_amd/csrc/qr_gi.h: an explicit H^-1-orthonormal basis of the active normals, numpy
+    statement scripts/qr_gi.py). Where the oracle fails, a GPU solution carries the level-1 KKT
+    certificate (1e-9) and the level-0 LSI certificate at 1e-8: those are the degenerate instances
+    (the oracle's own dual loop ends numerically there), where the final point's waist value carries
+    the level-0 step's roundoff (observed 2e-9)."""
     import kkt
     n, nc = 12, 4
     tot = dict(solved=0, repaired=0, miss=0, extra=0, l0_worst=0.0)
@@ -131,4 +125,4 @@ def test_contact_level0_repair_friction(wbq_mod, oracle_lib, mu):
                 (seed, b, l0, c)
     print("friction level-0 repair sweep:", tot)
     assert tot["repaired"] >= 500, tot  # the friction-aware repair path really runs
-    assert tot["miss"] <= FRICTION_MAX_MISS, tot
+    assert tot["miss"] == 0, tot
