@@ -89,3 +89,43 @@ def test_dual_qp_small_known_answer(oracle_lib):
     x, st, _ = oracle_lib.dual_qp(H, g, np.zeros((0, 2)), np.zeros(0),
                                   np.array([[1.0, 0.0], [1.0, 0.0]]), np.array([3.0, -10]), np.array([10.0, 2.0]))
     assert st == 2
+
+
+def test_qr_form_loop_matches_oracle(oracle_lib):
+    """The numpy statement of the repair kernel's QR-form fallback (scripts/qr_gi.py solve_metric,
+    qppvm_amd/csrc/qr_gi.h) on the friction sweep's level-1 problems (n = 12, nc = 4, mu = 0.5, torque
+    rows): solved from x0 alone -- and after the level-0 LSI with its pins where the waist is not
+    attainable -- it returns the oracle's tau on every instance the oracle solves (one seed here; the
+    20-seed sweep: 2,504 / 2,504)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import emulate_dual_gi as E
+    import qr_gi
+    from qppvm_amd.synth import contact_instances
+    masks = [0b0011, 0b0111, 0b1111, 0b0101, 0b1010, 0b1100]
+    n, nc, mu = 12, 4, 0.5
+    free = ContactProblem(n=n, nc=nc, mu=mu)
+    inp = contact_instances(free, 64, seed=101, masks=masks)
+    tf = oracle_lib.contact_batch(free, inp)[0]
+    prob = ContactProblem(n=n, nc=nc, mu=mu, torque_rows=True, tau_max=float(np.quantile(np.abs(tf[:, 6:]), 0.4)))
+    tau_r, _, st_r, _, _ = oracle_lib.contact_batch(prob, inp)
+    checked = 0
+    for b in range(64):
+        if st_r[b] != 0:
+            continue
+        P = E.Problem(prob, inp, b)
+        Hi = np.linalg.inv(P.H)
+        st, x, _ = qr_gi.solve_metric(Hi, P.x0, P.A, P.lo, P.hi, P.kind)
+        if st != 0:
+            lo, hi, wkeep = E.level0(P, prob, inp, b)
+            kind = P.kind.copy()
+            for r in range(6):
+                if not (wkeep >> r) & 1:
+                    kind[P.NJ + r] = 0
+            st, x, _ = qr_gi.solve_metric(Hi, P.x0, P.A, lo, hi, kind)
+        assert st == 0, b
+        err = np.abs(P.tau(x) - tau_r[b]).max() / max(1.0, np.abs(tau_r[b]).max())
+        assert err <= 1e-6, (b, err)
+        checked += 1
+    assert checked >= 50
