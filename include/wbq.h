@@ -236,6 +236,16 @@ int wbq_get_timing_detail(wbq_ctx *ctx, double *solve_ms, double *kernel_ms, int
  * new context. */
 #define WBQ_OPT_INLINE_REPAIR 1
 #define WBQ_OPT_FUSED_ROLLOUT 2
+/*   WBQ_OPT_FOLLOWUP        QPPVM W1 = I, n <= 32: 1 (default) while the last solves needed no level-0 repair, a
+ *                           solve enqueues its fast kernel alone; if that solve does list a repair, it is
+ *                           completed (its repair kernel run, then synchronised) by the next call that reads
+ *                           outputs: wbq_sync, wbq_get_outputs, wbq_get_device_outputs, wbq_get_state,
+ *                           wbq_get_warmstart_hints (a later wbq_solve supersedes it). Not applied with
+ *                           caller-owned device outputs (wbq_set_outputs: a stream consumer reads them
+ *                           without a call), rollouts or the constraint-space stacks. 0: every solve enqueues
+ *                           its follow-up kernel, so its outputs are final in stream order.
+ *                           (env WBQ_FOLLOWUP) */
+#define WBQ_OPT_FOLLOWUP 3
 int wbq_set_option(wbq_ctx *ctx, int option, int value);
 void wbq_destroy(wbq_ctx *ctx);
 const char *wbq_last_error(const wbq_ctx *ctx);

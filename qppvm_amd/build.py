@@ -92,15 +92,23 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     hdrs = _headers()
     # the record is taken before compiling: an edit made while the build runs leaves it stale
     record = _digest(flags, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
-    objs = [os.path.join(objdir, os.path.splitext(s)[0] + "_" +
-                         _digest(flags, [os.path.join(CSRC, s)] + _headers(os.path.join(CSRC, s))) + ".o")
-            for s in SOURCES]
+    def tu_flags(src):
+        # an experiment define reaches only the translation units whose sources name its macro, so the
+        # others keep their cached objects
+        if not defines:
+            return flags
+        text = "".join(open(p).read() for p in [src] + _headers(src))
+        keep = [d for d in defines if d.split("=")[0] in text]
+        return _flags(diag, tuple(keep))
+    tus = [(os.path.join(CSRC, s), tu_flags(os.path.join(CSRC, s))) for s in SOURCES]
+    objs = [os.path.join(objdir, os.path.splitext(os.path.basename(src))[0] + "_" +
+                         _digest(fl, [src] + _headers(src)) + ".o")
+            for src, fl in tus]
     procs = []
-    for s, o in zip(SOURCES, objs):
-        src = os.path.join(CSRC, s)
+    for (src, fl), o in zip(tus, objs):
         if (not force or os.environ.get("WBQ_INCREMENTAL")) and os.path.exists(o):
             continue
-        cmd = flags + ["-c", src, "-o", o + ".tmp"]
+        cmd = fl + ["-c", src, "-o", o + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd)))

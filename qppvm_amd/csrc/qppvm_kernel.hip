@@ -40,18 +40,38 @@
 
 #include <math.h>
 
+// Fast-kernel schedule switches (round 5; the A/B builds set them, scripts/ab_bench.py):
+//   WBQ_FAST_GJ_CH / _UNI  block_gj's trailing-read chunk and one-form update (wbq_device.h)
+//   WBQ_FAST_Y_CH          Y = M G^T with the G rows read a chunk of columns ahead (0: as compiled)
+//   WBQ_FAST_EQ_EARLY      1: the Gram G G^T (J only) as per-lane outer products summed by DPP and its
+//                          factor before M is waited for; after the elimination only res = G (w - u_imp)
+//                          (six DPP sums) and the small solves remain. 2: the same sums (Gram and res in
+//                          one 27-wide DPP reduction) after the elimination, the factor in registers.
+//                          0: LDS dots after the elimination
+// (same box, config 1: chunk 4 + one-form update 127.5 -> 131.8 M QP/s, chunk 2 within noise of it; the
+// DPP equality block, mode 2, 124.5 alone and 129.3 with them, mode 1 106.9: not kept)
+#ifndef WBQ_FAST_GJ_CH
+#define WBQ_FAST_GJ_CH 4
+#endif
+#ifndef WBQ_FAST_GJ_UNI
+#define WBQ_FAST_GJ_UNI 1
+#endif
+#ifndef WBQ_FAST_Y_CH
+#define WBQ_FAST_Y_CH 0
+#endif
+#ifndef WBQ_FAST_EQ_EARLY
+#define WBQ_FAST_EQ_EARLY 0
+#endif
+
 namespace wbq {
 namespace {
-
-
-
 
 // Per-instance LDS layouts in doubles (T = ntasks and m0 are launch constants). Rows of
 // NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
 template <int NP>
 struct FastLayout {
     static constexpr int BS = kGjBS; // Gauss-Jordan pivot block
-    int JR, PN, RH, U, WV, QD, F, RES, GR, PS, SIZE;
+    int JR, PN, RH, U, WV, QD, F, RES, GR, PS, LF, SIZE;
     __host__ __device__ FastLayout(int T, int m0)
     {
         JR = 0;                  // J rows [T*6][NP]
@@ -64,7 +84,8 @@ struct FastLayout {
         RES = F + 6 * T;         // b0 - G u_imp [m0]
         GR = RES + m0;           // Gram G G^T, lower triangle [m0][kM0Max]
         PS = GR + m0 * kM0Max;   // poses [T][24]
-        SIZE = (PS + 24 * T + 1) & ~1;
+        LF = PS + 24 * T;        // factor of the Gram (WBQ_FAST_EQ_EARLY): packed L, then 1 / diag
+        SIZE = (LF + kM0Max * (kM0Max + 1) / 2 + kM0Max + 1) & ~1;
     }
 };
 
@@ -399,6 +420,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         const long e = e0 + sub;
         const bool valid = e < cnt;
         WBQ_STAMP(4);
+        WBQ_RTSTAMP(30);
         const long b = valid ? a.wl[e] : 0;
         const int n = a.n;
         const bool row = valid && i < n;
@@ -435,6 +457,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             }
         }
         WBQ_STAMP(7);
+        WBQ_RTSTAMP(31);
     }
 }
 
@@ -519,6 +542,14 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 // overhead of any follow-up kernel (scripts/launch_probe2.hip, launch_probe3.hip: registers, LDS,
 // scratch, kernarg size and a cold L2 do not change it); rocprofv3's ~5 us duration for it includes
 // the dispatch.
+// (diagnostic: WBQ_ROLL_REPAIR_NOINLINE puts the fused rollout's inline repair behind a call -- the
+// round-4 variant that faulted on MI355X)
+template <int NP, int M0>
+__device__ __noinline__ void repair_instance_call(const QppvmArgs &a, double *S, long b, int i, bool rep)
+{
+    repair_instance<NP, M0>(a, S, b, i, rep);
+}
+
 template <int NP, int M0>
 __device__ __noinline__ void repair_list(const QppvmArgs &a, int cnt)
 {
@@ -533,8 +564,10 @@ __device__ __noinline__ void repair_list(const QppvmArgs &a, int cnt)
         const bool valid = e < cnt;
         const long b = valid ? a.wl[a.B + e] : 0;
         WBQ_STAMP(8);
+        WBQ_RTSTAMP(28); // (the constant 100 MHz clock beside the shader-clock stamps: their ratio is the clock)
         __syncthreads(); // the previous instance's LDS is dead
         repair_instance<NP, M0>(a, S, b, i, valid);
+        WBQ_RTSTAMP(29);
     }
 }
 
@@ -601,6 +634,9 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
     // stream order, for the host's choice of the next solve's variant (FollowGrid)
     if constexpr (MERGED && INLREP && !ROLL)
         follow_publish(a.fg, a.work[(a.epoch ^ 1) * 2], a.work[(a.epoch ^ 1) * 2 + 1]);
+    // (on-demand follow-up: no follow-up kernel publishes the counts or clears the counters either)
+    if constexpr (MERGED && !INLREP && !ROLL)
+        if (a.self_book) follow_publish(a.fg, a.work[(a.epoch ^ 1) * 2], a.work[(a.epoch ^ 1) * 2 + 1]);
     WBQ_RTSTAMP(16);
     WBQ_STAMP(0);
 
@@ -716,21 +752,104 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
 #pragma unroll
         for (int r = 0; r < MR; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     }
+    constexpr int NT = M0 * (M0 + 1) / 2;
+    if constexpr (WBQ_FAST_EQ_EARLY == 1) {
+        // the Gram G G^T and its factor from J alone, while M is still in flight: lane i's column of the
+        // selected J rows, per-lane outer products, instance sums by DPP (no LDS round trips); every
+        // lane factors it (rank-revealing Cholesky, dependent rows get a zero column) and lane 0 keeps
+        // the Gram (GR, lower triangle) and the factor (LF) for after the elimination
+        double g[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) g[c] = (c < m0) ? S[L.JR + a.row_sel[c < m0 ? c : 0] * NP + i] : 0.0;
+        double gg[NT];
+#pragma unroll
+        for (int r = 0; r < M0; ++r)
+#pragma unroll
+            for (int c = 0; c <= r; ++c) gg[r * (r + 1) / 2 + c] = g[r] * g[c];
+        isum_vec<NP, NT>(gg);
+        double Lq[NT], ilq[M0];
+        double dmx = 0.0;
+#pragma unroll
+        for (int r = 0; r < M0; ++r) {
+#pragma unroll
+            for (int c = 0; c <= r; ++c) Lq[r * (r + 1) / 2 + c] = (r < m0) ? gg[r * (r + 1) / 2 + c] : 0.0;
+            dmx = fmax(dmx, Lq[r * (r + 1) / 2 + r]);
+        }
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            double dd = Lq[c * (c + 1) / 2 + c];
+#pragma unroll
+            for (int k = 0; k < c; ++k) dd = fma(-Lq[c * (c + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], dd);
+            const bool indep = c < m0 && dd > 1e-12 * dmx;
+            const double ic_ = indep ? frsq(dd) : 0.0;
+            ilq[c] = ic_;
+            Lq[c * (c + 1) / 2 + c] = dd * ic_;
+#pragma unroll
+            for (int r = c + 1; r < M0; ++r) {
+                double t = Lq[r * (r + 1) / 2 + c];
+#pragma unroll
+                for (int k = 0; k < c; ++k) t = fma(-Lq[r * (r + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], t);
+                Lq[r * (r + 1) / 2 + c] = t * ic_;
+            }
+        }
+        if (i == 0) {
+#pragma unroll
+            for (int r = 0; r < M0; ++r) {
+#pragma unroll
+                for (int c = 0; c <= r; ++c)
+                    if (r < m0) S[L.GR + r * kM0Max + c] = gg[r * (r + 1) / 2 + c];
+                S[L.LF + NT + r] = ilq[r];
+            }
+#pragma unroll
+            for (int q = 0; q < NT; ++q) S[L.LF + q] = Lq[q];
+        }
+    }
     // M (still streaming in during the forces): padding rows/columns past n -> identity
 #pragma unroll
     for (int r = 0; r < MR; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
     // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
     // never has to be read again (a re-read of M would double the HBM bytes of the solve)
     double Y[M0];
+    if constexpr (WBQ_FAST_Y_CH == 0) {
 #pragma unroll
-    for (int c = 0; c < M0; ++c) {
-        double v = 0.0;
-        if (c < m0) {
-            const int rr = a.row_sel[c];
+        for (int c = 0; c < M0; ++c) {
+            double v = 0.0;
+            if (c < m0) {
+                const int rr = a.row_sel[c];
 #pragma unroll
-            for (int j = 0; j < MR; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+                for (int j = 0; j < MR; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+            }
+            Y[c] = v;
         }
-        Y[c] = v;
+    } else {
+        // the same sums (j ascending per row), the G rows read WBQ_FAST_Y_CH columns ahead
+        constexpr int YC = WBQ_FAST_Y_CH, NYC = MR / YC;
+        static_assert(MR % YC == 0, "WBQ_FAST_Y_CH divides MR");
+        int rrs[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            rrs[c] = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0;
+            Y[c] = 0.0;
+        }
+        double gb[2][M0][YC];
+#pragma unroll
+        for (int ch = 0; ch <= NYC; ++ch) {
+            if (ch < NYC) {
+#pragma unroll
+                for (int c = 0; c < M0; ++c)
+#pragma unroll
+                    for (int u = 0; u < YC; ++u) gb[ch & 1][c][u] = S[L.JR + rrs[c] * NP + ch * YC + u];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (ch > 0) {
+#pragma unroll
+                for (int c = 0; c < M0; ++c)
+#pragma unroll
+                    for (int u = 0; u < YC; ++u)
+                        Y[c] = fma(A[(ch - 1) * YC + u], c < m0 ? gb[(ch - 1) & 1][c][u] : 0.0, Y[c]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     __syncthreads();
     WBQ_STAMP(1);
@@ -747,17 +866,69 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
         rhs[1 + t] = c; // J_t^T F_t
     }
-    bool notspd = block_gj<NP, 1 + TM, 8, MR>(A, rhs, n, i, S + L.PN, S + L.RH);
+    // (the chunked reads only where the columns leave registers for them: with 64 columns per lane they
+    // spilled, 0 -> 528 B of scratch)
+    constexpr int kGjCh = MR <= 40 ? WBQ_FAST_GJ_CH : 0;
+    bool notspd = block_gj<NP, 1 + TM, 8, MR, kGjCh, WBQ_FAST_GJ_UNI != 0>(A, rhs, n, i, S + L.PN, S + L.RH);
     const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
+    double gq[NT], resq[M0]; // (EQ_EARLY == 2) the Gram and res in registers
+    if constexpr (!WBQ_FAST_EQ_EARLY) {
 #pragma unroll
-    for (int t = 0; t < TM; ++t)
-        if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
-    __syncthreads();
+        for (int t = 0; t < TM; ++t)
+            if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
+        __syncthreads();
+    }
     WBQ_STAMP(2);
 
     // ------------------------------ 3. level-0 rows: G u = b0 in least distance from u_imp
     // res_a = b0_a - G_a u_imp = G_a (w_t(a) - u_imp), and the Gram G G^T: one dot per lane
-    {
+    if constexpr (WBQ_FAST_EQ_EARLY == 2) {
+        // res and the Gram by per-lane products (lane i's column of the selected J rows), one DPP
+        // reduction of the NT + M0 sums; no LDS round trip
+        double g[M0], v[NT + M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
+            g[c] = c < m0 ? S[L.JR + rr * NP + i] : 0.0;
+            double w = rhs[1];
+#pragma unroll
+            for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
+            v[NT + c] = g[c] * (w - u_imp);
+        }
+#pragma unroll
+        for (int r = 0; r < M0; ++r)
+#pragma unroll
+            for (int c = 0; c <= r; ++c) v[r * (r + 1) / 2 + c] = g[r] * g[c];
+        isum_vec<NP, NT + M0>(v);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) gq[q] = v[q];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) resq[c] = v[NT + c];
+        if (i < m0) { // (the repair path's b0 reads res from LDS)
+            double rv = 0.0;
+#pragma unroll
+            for (int c = 0; c < M0; ++c) rv = i == c ? resq[c] : rv;
+            S[L.RES + i] = rv;
+        }
+    } else if constexpr (WBQ_FAST_EQ_EARLY == 1) {
+        // (the Gram and its factor are in LDS since the stage) res by per-lane products and DPP sums
+        double rp[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
+            double w = rhs[1];
+#pragma unroll
+            for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
+            rp[c] = c < m0 ? S[L.JR + rr * NP + i] * (w - u_imp) : 0.0;
+        }
+        isum_vec<NP, M0>(rp);
+        if (i == 0) {
+#pragma unroll
+            for (int c = 0; c < M0; ++c)
+                if (c < m0) S[L.RES + c] = rp[c];
+        }
+        __syncthreads();
+    } else {
         const int npairs = m0 * (m0 + 1) / 2;
         for (int pp = i; pp < npairs + m0; pp += NP) {
             if (pp < m0) {
@@ -773,19 +944,31 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
                 S[L.GR + ra * kM0Max + ca] = dot4<MR>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
             }
         }
+        __syncthreads();
     }
-    __syncthreads();
     // Every lane factors the small Gram redundantly in registers: rank-revealing Cholesky
     // G G^T = L L^T (dependent rows get a zero column), c = L^-T L^-1 res, u = u_imp + G^T c.
     double Lm[M0 * (M0 + 1) / 2]; // packed lower triangle, row-major
     double il[M0], rs[M0];
-    {
-        double dmx = 0.0;
+    if constexpr (WBQ_FAST_EQ_EARLY == 1) {
 #pragma unroll
         for (int r = 0; r < M0; ++r) {
             rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
+            il[r] = S[L.LF + NT + r];
+        }
 #pragma unroll
-            for (int c = 0; c <= r; ++c) Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
+        for (int q = 0; q < NT; ++q) Lm[q] = S[L.LF + q];
+    } else {
+        double dmx = 0.0;
+#pragma unroll
+        for (int r = 0; r < M0; ++r) {
+            if constexpr (WBQ_FAST_EQ_EARLY == 2) rs[r] = (r < m0) ? resq[r] : 0.0;
+            else rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
+#pragma unroll
+            for (int c = 0; c <= r; ++c) {
+                if constexpr (WBQ_FAST_EQ_EARLY == 2) Lm[r * (r + 1) / 2 + c] = (r < m0) ? gq[r * (r + 1) / 2 + c] : 0.0;
+                else Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
+            }
             dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
         }
 #pragma unroll
@@ -828,8 +1011,13 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
     for (int r = 0; r < M0; ++r) {
         double v = -rs[r];
 #pragma unroll
-        for (int c = 0; c < M0; ++c)
-            if (r < m0 && c < m0) v = fma(S[L.GR + (r >= c ? r * kM0Max + c : c * kM0Max + r)], cv[c], v);
+        for (int c = 0; c < M0; ++c) {
+            if constexpr (WBQ_FAST_EQ_EARLY == 2) {
+                if (r < m0 && c < m0) v = fma(gq[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r], cv[c], v);
+            } else {
+                if (r < m0 && c < m0) v = fma(S[L.GR + (r >= c ? r * kM0Max + c : c * kM0Max + r)], cv[c], v);
+            }
+        }
         eqres = fmax(eqres, fabs(v));
         rmx = fmax(rmx, fabs(rs[r]));
     }
@@ -945,6 +1133,12 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
         }
     }
     WBQ_STAMP(5);
+    if constexpr (MERGED && !INLREP && !ROLL) {
+        if (a.self_book && blockIdx.x == 0 && tid == 0) { // the next solve's counters (published above)
+            a.work[(a.epoch ^ 1) * 2] = 0;
+            a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+        }
+    }
     if constexpr (MERGED && INLREP) {
         // one launch per solve: no follow-up kernel resets the next solve's work counters
         if (!ROLL && blockIdx.x == 0 && tid == 0) {
@@ -957,6 +1151,10 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
         if (__any(rep_inl)) {
             if (!ROLL && rep_inl && i == 0) atomicAdd(a.work + a.epoch * 2 + 1, 1); // the repair count (grid policy)
             __syncthreads();
+#ifdef WBQ_ROLL_REPAIR_NOINLINE
+            if constexpr (ROLL) repair_instance_call<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
+            else
+#endif
             repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
         }
     }
@@ -1065,6 +1263,7 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     }
     // follow-up kernels: grid-stride over their work lists, grids sized from the last counts seen
     if (MERGED && kInlineRepair<M0> && a.inline_repair && !a.prepare) return hipSuccess; // repaired in the fast kernel
+    if (MERGED && a.skip_followup && !a.prepare) return hipSuccess; // on demand: the host completes it
     const unsigned g1 = follow_blocks(a.fg.est[1], IPW, kFollowGrid, a.B);
     if constexpr (MERGED) {
         return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
@@ -1077,6 +1276,16 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 }
 
 }  // namespace
+
+hipError_t launch_qppvm_followup(const QppvmArgs &a, hipStream_t stream)
+{
+    // (the NP = 32 merged path only: its one follow-up is the repair kernel)
+    if (a.n > 32 || a.B <= 0) return hipErrorInvalidValue;
+    const unsigned g1 = follow_blocks(a.fg.est[1], 2, kFollowGrid, a.B);
+    if (a.m0 <= 6 && a.m_l0 >= a.m0)
+        return launch_one<32, ActiveLayout<32>>(qppvm_repair_kernel<32, 6>, a, g1, stream);
+    return launch_one<32, ActiveLayout<32>>(qppvm_repair_kernel<32, kM0Max>, a, g1, stream);
+}
 
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
 {

@@ -1152,6 +1152,9 @@ __device__ __forceinline__ void wl_push(const QppvmArgs &a, int list, long b)
 {
     const int idx = atomicAdd(&a.work[a.epoch * 2 + list], 1);
     a.wl[(long)list * a.B + idx] = (int)b;
+    // (the host's completion check of an on-demand solve: some instance waits for the repair kernel)
+    if (list == 1 && a.self_book && a.fg.seen)
+        __hip_atomic_store(a.fg.seen + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Follow-up grid cap: 2 waves per SIMD over the whole chip (launch cost measured independent of

@@ -86,6 +86,10 @@ struct wbq_ctx {
     // per-context options (wbq_set_option); the environment gives a new context's initial values
     int opt_inline = env_option("WBQ_INLREP", -1); // WBQ_OPT_INLINE_REPAIR
     int opt_fused = env_option("WBQ_FUSED_ROLLOUT", 1); // WBQ_OPT_FUSED_ROLLOUT
+    int opt_followup = env_option("WBQ_FOLLOWUP", 1);  // WBQ_OPT_FOLLOWUP
+    // on-demand follow-up: the last solve skipped its repair kernel; completed when outputs are read
+    bool pending = false;
+    wbq::QppvmArgs pend_args{};
     // follow-up grid sizing (wbq_kernels.h FollowGrid): counts the last follow-up kernel saw, in
     // mapped pinned host memory (device view work_seen_dev), and the host's running estimate
     int *work_seen = nullptr, *work_seen_dev = nullptr;
@@ -180,9 +184,9 @@ wbq::FollowGrid follow_grid(wbq_ctx *c)
 
 bool alloc_work_seen(wbq_ctx *c)
 {
-    if (hipHostMalloc((void **)&c->work_seen, 2 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    if (hipHostMalloc((void **)&c->work_seen, 3 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return false;
-    c->work_seen[0] = c->work_seen[1] = 0;
+    c->work_seen[0] = c->work_seen[1] = c->work_seen[2] = 0;
     return hipHostGetDevicePointer((void **)&c->work_seen_dev, c->work_seen, 0) == hipSuccess;
 }
 
@@ -276,6 +280,8 @@ int solve_contact(wbq_ctx *c, int integrate, double dt, bool prepare, const wbq_
 extern "C" {
 
 const char *wbq_version(void) { return kVersion; }
+
+static int complete_pending(wbq_ctx *c); // (an on-demand solve is finished before its state changes)
 
 const char *wbq_last_error(const wbq_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
@@ -522,6 +528,7 @@ int wbq_get_contact_outputs(wbq_ctx *c, double *x)
 int wbq_set_stream(wbq_ctx *c, void *hip_stream)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
     return WBQ_SUCCESS;
 }
@@ -529,6 +536,7 @@ int wbq_set_stream(wbq_ctx *c, void *hip_stream)
 int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
 {
     if (!c || !in) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE; // (its repair reads the current inputs)
     if (c->form != WBQ_FORM_QPPVM) return fail(c, WBQ_E_INVALID, "wbq_set_inputs on a contact-form context");
     if (in->batch < 0 || in->batch > c->d.max_batch)
         return fail(c, WBQ_E_CAPACITY, "batch exceeds max_batch");
@@ -646,6 +654,16 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
         if (seen1 > 0) c->inl_hold = 64;
         else if (c->inl_hold > 0) --c->inl_hold;
         a.inline_repair = c->opt_inline >= 0 ? c->opt_inline : (c->inl_hold > 0 ? 1 : 0);
+        // On-demand follow-up (WBQ_OPT_FOLLOWUP): while the last solves listed no repair, the n <= 32
+        // merged path enqueues the fast kernel alone (an empty follow-up launch costs ~1.5-3 us of a
+        // ~35 us config-1 step); a solve that did list one is completed when its outputs are read
+        // (complete_pending). Not with caller-owned device outputs (a stream consumer would read them
+        // before that), rollouts, rbd re-evaluation, or the constraint-space and inline variants.
+        a.skip_followup = (c->opt_followup == 1 && !prepare && !integrate && steps == 0 && !rbd && a.B > 0 &&
+                           c->d.n <= 32 && c->d.joint_weight == WBQ_WEIGHT_IDENTITY && !c->d.no_joint_task &&
+                           !a.inline_repair && !c->out_tau && !c->out_status && !c->out_iters && seen1 == 0 &&
+                           c->fest[1] == 0) ? 1 : 0;
+        a.self_book = a.skip_followup;
     }
 
     WBQ_HIP(hipSetDevice(c->device));
@@ -662,6 +680,9 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
                                 const_cast<double *>(c->in[7]), const_cast<double *>(c->in[1]),
                                 const_cast<double *>(c->in[2]), c->stream));
     WBQ_HIP(wbq::launch_qppvm(a, c->stream, timed ? c->ev[c->ev_used + 1] : nullptr));
+    // (a skipped solve's predecessor, if it was pending, is superseded: its outputs are overwritten)
+    c->pending = a.skip_followup != 0;
+    if (c->pending) c->pend_args = a;
     if (a.B > 0) c->epoch ^= 1; // solves on one context are stream-ordered
     if (timed) {
         WBQ_HIP(hipEventRecord(c->ev[c->ev_used + 2], c->stream));
@@ -685,6 +706,11 @@ int wbq_set_option(wbq_ctx *c, int option, int value)
         if (value < 0 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_FUSED_ROLLOUT: 0 or 1");
         c->opt_fused = value;
         return WBQ_SUCCESS;
+    case WBQ_OPT_FOLLOWUP:
+        if (value < 0 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_FOLLOWUP: 0 or 1");
+        if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
+        c->opt_followup = value;
+        return WBQ_SUCCESS;
     default:
         return fail(c, WBQ_E_INVALID, "wbq_set_option: unknown option");
     }
@@ -693,6 +719,7 @@ int wbq_set_option(wbq_ctx *c, int option, int value)
 int wbq_rollout(wbq_ctx *c, int steps, double dt)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (steps < 0 || !(dt >= 0.0)) return fail(c, WBQ_E_INVALID, "wbq_rollout: steps >= 0, dt >= 0");
     if (c->form == WBQ_FORM_QPPVM && c->d.no_joint_task)
         return fail(c, WBQ_E_UNSUPPORTED, "wbq_rollout: not with no_joint_task (qdd = M^-1 x is not carried)");
@@ -711,6 +738,7 @@ int wbq_rollout(wbq_ctx *c, int steps, double dt)
 int wbq_rollout_rbd(wbq_ctx *c, wbq_rbd_ctx *rbd, int steps, double dt)
 {
     if (!c || !rbd) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
     const int want_t = c->form == WBQ_FORM_CONTACT ? 1 + c->cd.nc : c->d.ntasks;
     if (wbq::rbd_n(rbd) != c->d.n || wbq::rbd_ntasks(rbd) != want_t || wbq::rbd_device(rbd) != c->device)
@@ -736,6 +764,7 @@ int wbq_rollout_rbd(wbq_ctx *c, wbq_rbd_ctx *rbd, int steps, double dt)
 int wbq_get_state(wbq_ctx *c, double *q, double *qd)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
     if (c->batch == 0) return WBQ_SUCCESS;
     WBQ_HIP(hipSetDevice(c->device));
@@ -751,6 +780,7 @@ int wbq_get_state(wbq_ctx *c, double *q, double *qd)
 int wbq_set_state(wbq_ctx *c, const double *q, const double *qd, int memory)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (!c->have_inputs) return fail(c, WBQ_E_INVALID, "no inputs set");
     if (memory != WBQ_MEM_DEVICE && memory != WBQ_MEM_HOST) return fail(c, WBQ_E_INVALID, "unknown memory kind");
     if (c->batch == 0) return WBQ_SUCCESS;
@@ -765,9 +795,31 @@ int wbq_set_state(wbq_ctx *c, const double *q, const double *qd, int memory)
     return WBQ_SUCCESS;
 }
 
+// An on-demand solve (WBQ_OPT_FOLLOWUP) whose fast kernel listed instances for the level-0 repair is
+// finished here, before any of its outputs are read: the flag the listing set in mapped host memory,
+// then the repair kernel over that solve's list. A solve that listed none costs one host read.
+static int complete_pending(wbq_ctx *c)
+{
+    if (!c->pending) return WBQ_SUCCESS;
+    c->pending = false;
+    WBQ_HIP(hipSetDevice(c->device));
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    if (c->work_seen && __atomic_load_n(c->work_seen + 2, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(c->work_seen + 2, 0, __ATOMIC_RELEASE);
+        wbq::QppvmArgs a = c->pend_args;
+        a.skip_followup = 0;
+        a.self_book = 0;
+        a.fg = follow_grid(c);
+        WBQ_HIP(wbq::launch_qppvm_followup(a, c->stream));
+        WBQ_HIP(hipStreamSynchronize(c->stream));
+    }
+    return WBQ_SUCCESS;
+}
+
 int wbq_sync(wbq_ctx *c)
 {
     if (!c) return WBQ_E_INVALID;
+    if (c->pending) return complete_pending(c);
     WBQ_HIP(hipStreamSynchronize(c->stream));
     return WBQ_SUCCESS;
 }
@@ -775,6 +827,7 @@ int wbq_sync(wbq_ctx *c)
 int wbq_get_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     WBQ_HIP(hipSetDevice(c->device));
     const size_t B = (size_t)c->batch, n = (size_t)c->d.n;
     if (B == 0) return WBQ_SUCCESS;
@@ -798,6 +851,7 @@ int wbq_get_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
 int wbq_set_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE; // (the last solve wrote the old buffers)
     c->out_tau = tau;
     c->out_status = status;
     c->out_iters = iters;
@@ -807,6 +861,7 @@ int wbq_set_outputs(wbq_ctx *c, double *tau, int32_t *status, int32_t *iters)
 int wbq_get_device_outputs(wbq_ctx *c, const double **tau, const int32_t **status, const int32_t **iters)
 {
     if (!c) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE; // (then valid on the stream as well)
     if (tau) *tau = c->out_tau ? c->out_tau : c->tau;
     if (status) *status = c->out_status ? c->out_status : c->status;
     if (iters) *iters = c->out_iters ? c->out_iters : c->iters;
@@ -842,6 +897,7 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
 int wbq_get_warmstart_hints(wbq_ctx *c, uint8_t *hints)
 {
     if (!c || !hints) return WBQ_E_INVALID;
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (c->batch == 0) return WBQ_SUCCESS;
     if (!c->ws_hint) {
         std::memset(hints, 0, (size_t)c->batch);

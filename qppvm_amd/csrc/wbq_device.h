@@ -386,6 +386,21 @@ __device__ double cart_error_component(const double *P, const double *Pr, int r)
 // rows within 0.5 %, 8 rows 28 % slower (the 8 x 8 pivot Cholesky chain and its registers)
 constexpr int kGjBS = 4;
 
+// Trailing-update read schedule (round 5): the panel entries of CH columns are read a chunk ahead of
+// their FMAs (two chunks in registers). The compiler's own schedule kept one ds_read_b128 in flight and
+// waited for it before the next: the elimination ran at the LDS latency (a lone wave's 8 steps took 16k
+// cycles). 0 = the compiler's schedule.
+#ifndef WBQ_GJ_CH
+#define WBQ_GJ_CH 0
+#endif
+// One update form for every row (round 5): row_i += hh . row_P with hh = D^-1 e_ri - e_ri for the
+// pivot block's own rows (row_i - row_P[ri] + (D^-1 row_P)[ri], the normalised pivot row to roundoff)
+// and hh = -D^-1 a_i elsewhere, instead of cc * row_i with cc = 0 / 1: one v_mul_f64 less per column
+// and step. 0 = the cc form.
+#ifndef WBQ_GJ_UNI
+#define WBQ_GJ_UNI 0
+#endif
+
 // Pivot blocks of BS = 4 rows. M is SPD, so no pivoting is needed and the trailing Schur
 // complement stays symmetric: pivot row k+r, column j, equals lane j's entry in column k+r.
 // Every lane publishes its BS panel entries; every lane factors the BS x BS pivot block D
@@ -396,7 +411,7 @@ constexpr int kGjBS = 4;
 // NC (a multiple of BS, n <= NC <= NP): the columns held per lane. Lanes i >= NC and columns past
 // NC are identity / zero and never pivoted, so an instantiation for n <= 40 in 64 lanes carries
 // 40 columns instead of 64 (the n = 39 fast kernel: 48 fewer VGPRs, 40 % less update work).
-template <int NP, int NR, int RHS, int NC = NP>
+template <int NP, int NR, int RHS, int NC = NP, int CH = WBQ_GJ_CH, bool UNI = (WBQ_GJ_UNI != 0)>
 __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int n, int i, double *PN, double *RH)
 {
     static_assert(NC % kGjBS == 0 && NC <= NP, "block_gj: NC");
@@ -425,6 +440,13 @@ __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int
             for (int r = 0; r < BS; ++r)
 #pragma unroll
                 for (int c = 0; c <= r; ++c) d[r][c] = pn[(k + r) * BS + c];
+            double la[BS][BS]; // (CH > 0) the lookahead panel, read with the pivot block
+            if constexpr (CH > 0) {
+#pragma unroll
+                for (int u = 0; u < BS; ++u)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) la[u][c] = (k + BS + u < NC) ? pn[(k + BS + u) * BS + c] : 0.0;
+            }
             double il[BS];
 #pragma unroll
             for (int c = 0; c < BS; ++c) {
@@ -462,10 +484,10 @@ __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int
             const double cc = inK ? 0.0 : 1.0;
             double hh[BS];
 #pragma unroll
-            for (int c = 0; c < BS; ++c) hh[c] = inK ? y[c] : -y[c];
+            for (int c = 0; c < BS; ++c) hh[c] = UNI ? (inK ? y[c] - (ri == c ? 1.0 : 0.0) : -y[c]) : (inK ? y[c] : -y[c]);
 #pragma unroll
             for (int m = 0; m < NR; ++m) {
-                double v = cc * rhs[m];
+                double v = UNI ? rhs[m] : cc * rhs[m];
 #pragma unroll
                 for (int c = 0; c < BS; ++c) v = fma(hh[c], rh[c * RHS + m], v);
                 rhs[m] = v;
@@ -473,9 +495,9 @@ __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int
             // lookahead: next panel first
 #pragma unroll
             for (int j = k + BS; j < k + 2 * BS && j < NC; ++j) {
-                double v = cc * A[j];
+                double v = UNI ? A[j] : cc * A[j];
 #pragma unroll
-                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                for (int c = 0; c < BS; ++c) v = fma(hh[c], CH > 0 ? la[j - k - BS][c] : pn[j * BS + c], v);
                 A[j] = v;
             }
             if (k + BS < n) {
@@ -490,12 +512,43 @@ __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int
                     for (int m = 0; m < NR; ++m) rhn[rn * RHS + m] = rhs[m];
                 }
             }
+            if constexpr (CH == 0) {
 #pragma unroll
-            for (int j = k + 2 * BS; j < NC; ++j) {
-                double v = cc * A[j];
+                for (int j = k + 2 * BS; j < NC; ++j) {
+                    double v = UNI ? A[j] : cc * A[j];
 #pragma unroll
-                for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
-                A[j] = v;
+                    for (int c = 0; c < BS; ++c) v = fma(hh[c], pn[j * BS + c], v);
+                    A[j] = v;
+                }
+            } else {
+                // trailing columns in chunks of CH: the next chunk's reads issue before this chunk's FMAs
+                constexpr int NCH = (NC + CH - 1) / CH;
+                double pv[2][CH][BS];
+#pragma unroll
+                for (int ch = 0; ch <= NCH; ++ch) {
+                    const int j0 = k + 2 * BS + ch * CH;
+                    if (ch < NCH && j0 < NC) {
+#pragma unroll
+                        for (int u = 0; u < CH; ++u)
+#pragma unroll
+                            for (int c = 0; c < BS; ++c) pv[ch & 1][u][c] = (j0 + u < NC) ? pn[(j0 + u) * BS + c] : 0.0;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int jp = j0 - CH;
+                    if (ch > 0 && jp < NC) {
+#pragma unroll
+                        for (int u = 0; u < CH; ++u) {
+                            const int j = jp + u;
+                            if (j < NC) {
+                                double v = UNI ? A[j] : cc * A[j];
+#pragma unroll
+                                for (int c = 0; c < BS; ++c) v = fma(hh[c], pv[(ch - 1) & 1][u][c], v);
+                                A[j] = v;
+                            }
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
     }

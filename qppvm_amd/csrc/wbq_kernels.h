@@ -17,7 +17,8 @@ constexpr int kM0Max = 12;  // level-0 rows handled by the kernel
 // profiles/r02_v15_kernel_stats.csv). The grid size never changes a result: every block loops
 // over the list until it is drained.
 struct FollowGrid {
-    int *seen;    // [2] mapped host memory: counts of the two lists at the last follow-up launch
+    int *seen;    // [3] mapped host memory: counts of the two lists at the last follow-up launch; [2] set
+                  // when an instance joins the repair list (the on-demand follow-up's completion check)
     int est[2];   // host estimate of this solve's counts (work items, not blocks)
 };
 constexpr unsigned kFollowMin = 16; // blocks: a count that grows from an estimate of 0 still has 16 waves
@@ -106,6 +107,12 @@ struct QppvmArgs {
     // 32, M0 <= 6): every wave carries its instances through all steps, so an instance that needs a
     // long level-0 repair in some step holds only its own wave, not every instance's next step
     int steps;
+    // on-demand follow-up (WBQ_OPT_FOLLOWUP, NP = 32 merged path): skip_followup = the launcher does not
+    // enqueue qppvm_repair_kernel after the fast kernel (the host completes a solve that listed repairs
+    // when its outputs are read); self_book = the fast kernel then does the follow-up kernel's
+    // bookkeeping itself (publishes the previous solve's counts, clears the next solve's counters)
+    int skip_followup;
+    int self_book;
 };
 
 // The box on x = tau - h of joint j (QPPVMPlugin.cpp:203-205: tau limits shifted by -h; with the
@@ -123,7 +130,7 @@ __device__ __forceinline__ void torque_box(const QppvmArgs &a, int j, double q, 
     hi = u - h;
 }
 
-constexpr int kStamps = 28; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7; repair 8-12; BVLS split 20-27
+constexpr int kStamps = 32; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7 (+30,31); repair 8-12 (+28,29); BVLS split 20-27
 
 // Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
 // device and kernel; thread-safe: contexts on several devices or threads share it). Called only
@@ -133,6 +140,8 @@ hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes);
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
 // mid (optional): recorded on the stream right after the first (dominant) kernel.
 hipError_t launch_qppvm(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
+// The follow-up repair kernel alone for a solve launched with skip_followup (its epoch's list).
+hipError_t launch_qppvm_followup(const QppvmArgs &a, hipStream_t stream);
 // W1 = M (joint_weight 1): main kernel + level-0 repair kernel; needs m0 + n <= 64
 hipError_t launch_qppvm_w1m(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid = nullptr);
 

@@ -248,6 +248,7 @@ class QPPVMSolver:
 
     OPT_INLINE_REPAIR = 1  # include/wbq.h WBQ_OPT_*
     OPT_FUSED_ROLLOUT = 2
+    OPT_FOLLOWUP = 3  # on-demand follow-up kernel (completed when outputs are read)
 
     def set_option(self, option: int, value: int):
         """Per-context execution option (wbq_set_option): a path choice, never a result change."""

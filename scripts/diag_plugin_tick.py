@@ -34,7 +34,7 @@ def main():
     wbq.load_library(lib)
     s = wbq.QPPVMSolver(prob, max_batch=1)
     s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    K = 28
+    K = 32
     rows = []
     for t in range(ticks):
         inp = {k: np.ascontiguousarray(d[k][t:t + 1]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
@@ -53,6 +53,19 @@ def main():
         rep = st[12] > st[8]
         row = {"tick": t, "us": 1e3 * ms, "status": int(status[0]), "iters": int(iters[0]), "repair": bool(rep),
                "fast_cycles": int(st[5] - st[0])}
+        # the constant 100 MHz clock (s_memrealtime, global): where the tick's device time goes, and the
+        # shader clock each phase ran at (s_memtime cycles / realtime)
+        t0 = st[16]
+        row["rt_us"] = {"fast": (st[17] - st[16]) / 100.0}
+        if st[31] > st[30] > 0:
+            row["rt_us"]["active"] = (st[31] - st[30]) / 100.0
+            row["rt_us"]["fast_end_to_active"] = (st[30] - st[17]) / 100.0
+        if rep and st[29] > st[28] > 0:
+            row["rt_us"]["repair"] = (st[29] - st[28]) / 100.0
+            row["rt_us"]["before_repair"] = (st[28] - (st[31] if st[31] > st[30] > 0 else st[17])) / 100.0
+            row["rt_us"]["span"] = (st[29] - t0) / 100.0
+            row["repair_clock_ghz"] = (st[12] - st[8]) / max(1.0, (st[29] - st[28]) / 100.0) / 1e3
+        row["fast_clock_ghz"] = (st[5] - st[0]) / max(1.0, (st[17] - st[16]) / 100.0) / 1e3
         if rep:
             row.update({"gj": int(st[9] - st[8]), "bvls": int(st[10] - st[9]), "pins_eq": int(st[11] - st[10]),
                         "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14]),
@@ -63,6 +76,15 @@ def main():
     us = np.array([r["us"] for r in rows])
     print(json.dumps({"ticks": ticks, "us_p50_p90_p99_max": [float(np.percentile(us, q)) for q in (50, 90, 99, 100)],
                       "repair_share": float(np.mean([r["repair"] for r in rows]))}))
+    # stamped time vs device time: the share of each tick the realtime stamps account for
+    acc = [sum(v for k, v in r["rt_us"].items() if k in ("fast", "active", "repair", "fast_end_to_active", "before_repair"))
+           / r["us"] for r in rows if r["repair"] and "repair" in r["rt_us"]]
+    if acc:
+        print(json.dumps({"repaired_ticks": len(acc), "realtime_span_over_device_time_p10_p50_p90":
+                          [float(np.percentile(acc, q)) for q in (10, 50, 90)],
+                          "repair_clock_ghz_p10_p50_p90": [float(np.percentile([r["repair_clock_ghz"] for r in rows
+                                                                                 if "repair_clock_ghz" in r], q))
+                                                           for q in (10, 50, 90)]}))
     for r in sorted(rows, key=lambda r: -r["us"])[:8]:
         print(json.dumps(r))
 
