@@ -152,6 +152,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     const int n = a.n, m0 = a.m0;
     const ActiveLayout<NP> L(a.ntasks, m0);
     const int ic = i < n ? i : n - 1;
+    WBQ_LAP_INIT; // (diagnostic build: cycles per phase of the loop, stamp slots 20-27, counts 13-14)
     // M rows (columns, coalesced); 64-bit addressing: the instances of a wave come from a work
     // list here, so no wave-uniform base exists for a buffer resource
     const double *Mb = a.M + b * n * n + ic;
@@ -189,6 +190,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     const bool eqb = lo == hi;
     infeasible = false;
     __syncthreads();
+    WBQ_LAP(0);
     if (__any(go && row && wsg != 0)) {
         // ------------------------------------------------ warm start: the last active set in one batch
         const bool wme = go && row && wsg != 0;
@@ -225,6 +227,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             }
             __syncthreads();
         }
+        WBQ_LAP(1);
         // residuals r_a = beta_a - n_a . u on the slot lanes, w = T^T r (lane j: w_j), lambda = T w
         const double s0 = Mr.dot(S + L.U, NP);
         const double xp = __shfl(s0, myp, NP), lop = __shfl(lo, myp, NP), hip = __shfl(hi, myp, NP);
@@ -265,6 +268,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         __syncthreads();
         S[L.U + i] = u_i;
         __syncthreads();
+        WBQ_LAP(2);
     }
     while (true) {
         const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
@@ -283,6 +287,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             lamp = 0.0;
         }
         if (!__any(go)) break;
+        WBQ_LAP_ADD(0, 1);
         const double s_p = __shfl(s_i, p, NP);
         const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
         const double npn = __shfl(nrm, p, NP);
@@ -290,8 +295,10 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
         S[L.NV + i] = npj;
         __syncthreads();
+        WBQ_LAP(3);
         const double z = project_out<NP>(S, L, npj, q, i);
         const double zz = isum<NP>(z * z);
+        WBQ_LAP(4);
         double ra = 0.0;
         if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
         const double rmax = imax<NP>(fabs(ra));
@@ -353,6 +360,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         }
         S[L.U + i] = u_i;
         __syncthreads();
+        WBQ_LAP(5);
         if (__any(rebuild)) {
             // Re-factor the inequality directions from the dropped position on: Q1T rows
             // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
@@ -386,9 +394,12 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                     ++q;
                 }
                 __syncthreads();
+                WBQ_LAP_ADD(1, 1);
             }
+            WBQ_LAP(6);
         }
     }
+    WBQ_LAP(3); // (the last pass: select only)
     if (record) { // the final active set, by joint, for the next solve of this instance
         S[L.NV + i] = 0.0;
         __syncthreads();
@@ -399,7 +410,10 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         if (go_rec(row, b, a)) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
         __syncthreads();
     }
-    return Mr.dot(S + L.U, NP);
+    const double xf = Mr.dot(S + L.U, NP);
+    WBQ_LAP(7);
+    WBQ_LAP_FLUSH(20, 13);
+    return xf;
 }
 
 // Active-set kernel (NP = 64; NP = 32 runs it inline in the fast kernel): instances parked
@@ -1151,11 +1165,22 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
         if (__any(rep_inl)) {
             if (!ROLL && rep_inl && i == 0) atomicAdd(a.work + a.epoch * 2 + 1, 1); // the repair count (grid policy)
             __syncthreads();
+#ifdef WBQ_STAMPS
+            const unsigned long long rt0_ = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef WBQ_ROLL_REPAIR_NOINLINE
             if constexpr (ROLL) repair_instance_call<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
             else
 #endif
             repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
+#ifdef WBQ_STAMPS
+            // (diagnostic: inline repairs' cycles and count summed in slots 6 / 7)
+            const unsigned long long rt1_ = __builtin_amdgcn_s_memtime();
+            if (tid == 0 && a.stamps) {
+                a.stamps[blockIdx.x * kStamps + 6] += rt1_ - rt0_;
+                a.stamps[blockIdx.x * kStamps + 7] += 1;
+            }
+#endif
         }
     }
     WBQ_RTSTAMP(17);
@@ -1181,6 +1206,8 @@ __global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
         a.work[(a.epoch ^ 1) * 2] = 0;
         a.work[(a.epoch ^ 1) * 2 + 1] = 0;
     }
+    WBQ_STAMP(28); // (diagnostic: the block's whole rollout, shader clock 28-29, realtime 30-31)
+    WBQ_RTSTAMP(30);
 #pragma unroll 1
     for (int s = 0; s < a.steps; ++s) {
         // the arguments through an opaque kernarg pointer per step: values loaded from them are not
@@ -1192,6 +1219,8 @@ __global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
         fast_body<NP, M0, true, TM, 2, 32, true, true>(as);
         __syncthreads(); // this wave's q, qd and warm-start writes are visible to its next step
     }
+    WBQ_STAMP(29);
+    WBQ_RTSTAMP(31);
 }
 
 template <int NP, typename Lay, typename K>

@@ -967,6 +967,13 @@ int wbq_diag_stamps(wbq_ctx *c, unsigned long long *host, int nblocks)
                       hipMemcpyDeviceToHost));
     return WBQ_SUCCESS;
 }
+int wbq_diag_stamps_clear(wbq_ctx *c, int nblocks)
+{
+    if (!c || !c->stamps) return WBQ_E_INVALID;
+    WBQ_HIP(hipStreamSynchronize(c->stream));
+    WBQ_HIP(hipMemset(c->stamps, 0, sizeof(unsigned long long) * wbq::kStamps * nblocks));
+    return WBQ_SUCCESS;
+}
 #endif
 
 void wbq_destroy(wbq_ctx *c)

@@ -28,9 +28,35 @@ __device__ __forceinline__ double fin_abs(double v) { return fabs(v) < 1.0e299 ?
         __builtin_amdgcn_sched_barrier(0);                                              \
         if (threadIdx.x == 0 && a.stamps) a.stamps[blockIdx.x * kStamps + (k)] = t_;    \
     } while (0)
+// lap counters: cycles of a loop's phases summed over its iterations (WBQ_LAP_INIT, WBQ_LAP(k) ends
+// phase k, WBQ_LAP_ADD(k, v) adds a count), added to stamp slot k by WBQ_LAP_FLUSH (slots cleared by
+// wbq_diag_stamps_clear)
+#define WBQ_LAP_INIT                                                                    \
+    unsigned long long lap_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lap_cnt_[2] = {0, 0};     \
+    unsigned long long lap_t_ = __builtin_amdgcn_s_memtime()
+#define WBQ_LAP(k)                                                                      \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                     \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        lap_acc_[k] += t_ - lap_t_;                                                     \
+        lap_t_ = t_;                                                                    \
+    } while (0)
+#define WBQ_LAP_ADD(k, v) (lap_cnt_[k] += (v))
+#define WBQ_LAP_FLUSH(base, cbase)                                                      \
+    do {                                                                                \
+        if (threadIdx.x == 0 && a.stamps) {                                             \
+            for (int k_ = 0; k_ < 8; ++k_) a.stamps[blockIdx.x * kStamps + (base) + k_] += lap_acc_[k_]; \
+            for (int k_ = 0; k_ < 2; ++k_) a.stamps[blockIdx.x * kStamps + (cbase) + k_] += lap_cnt_[k_]; \
+        }                                                                               \
+    } while (0)
 #else
 #define WBQ_STAMP(k) do {} while (0)
 #define WBQ_RTSTAMP(k) do {} while (0)
+#define WBQ_LAP_INIT do {} while (0)
+#define WBQ_LAP(k) do {} while (0)
+#define WBQ_LAP_ADD(k, v) do {} while (0)
+#define WBQ_LAP_FLUSH(base, cbase) do {} while (0)
 #endif
 
 // Workgroup barrier that orders LDS only. __syncthreads() is a workgroup fence on every
