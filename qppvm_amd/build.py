@@ -74,9 +74,12 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False, defines: tuple = (),
-          out: str | None = None) -> str:
+          out: str | None = None, diag_tus: tuple | None = None) -> str:
     """diag=True builds libwbq_diag.so with in-kernel phase stamps (never the product);
-    defines/out build an experiment variant (scripts/ab_bench.py) at another path."""
+    defines/out build an experiment variant (scripts/ab_bench.py) at another path. diag_tus: stamp
+    only these translation units (plus wbq_api.hip, which holds the stamp buffers and the read-out),
+    the others link their product objects (the argument structs do not depend on the flag; a stamped
+    qppvm or contact unit compiles for ~25 min)."""
     if defines and out is None:
         raise ValueError("an experiment build (defines) needs its own output path: the product "
                          "library and its source stamp describe the product flags only")
@@ -93,6 +96,8 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, define
     # the record is taken before compiling: an edit made while the build runs leaves it stale
     record = _digest(flags, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
     def tu_flags(src):
+        if diag and diag_tus is not None and os.path.basename(src) not in tuple(diag_tus) + ("wbq_api.hip",):
+            return _flags(False, defines)
         # an experiment define reaches only the translation units whose sources name its macro, so the
         # others keep their cached objects
         if not defines:

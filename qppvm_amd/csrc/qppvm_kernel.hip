@@ -105,25 +105,36 @@ struct FastLdsLayout {
 // lanes that own a joint row of a valid instance store its warm side (ws_rows exists for W1 = I)
 __device__ __forceinline__ bool go_rec(bool row, long, const QppvmArgs &a) { return row && a.ws_rows; }
 
-// Orthogonalise the normal held in NV against the rows of Q1T (two classical Gram-Schmidt
-// passes). Rows >= q of Q1T are finite and D1[c >= q] = 0, so every loop runs to NP
-// unguarded. Leaves d1 = Q1^T n in D1 and returns this lane's entry of z.
+// Orthogonalise the normal held in NV against the rows of Q1T by classical Gram-Schmidt, a second
+// pass only where the first lost more than half the norm (|z|^2 <= |n|^2 / 2, "twice is enough":
+// after a pass that keeps |z| >= |n| / sqrt(2) the residual is orthogonal to roundoff; the loop's
+// normals, rows of M, rarely lean that far into the active span). Rows >= q of Q1T are finite and
+// D1[c >= q] = 0, so every loop runs to NP unguarded. Leaves d1 = Q1^T n in D1, |z|^2 in zz (every
+// lane of the instance) and returns this lane's entry of z. nn2 = |n|^2; act: the instance takes part
+// (the second pass runs for the whole wave when any taking part needs it: barriers stay uniform).
+// (Each pass is two LDS dot products per lane: with eight waves per CU in this loop the LDS port is
+// the bound, and the second pass was half of it.)
 template <int NP>
-__device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> &L, double npj, int q, int i)
+__device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> &L, double npj, int q, int i,
+                                              double nn2, bool act, double &zz)
 {
     constexpr int RS = NP + 1;
     const double d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
     S[L.D1 + i] = d1;
     __syncthreads();
     double z = npj - dot4s<NP>(S + L.QA + i, RS, S + L.D1);
-    S[L.BC + i] = z;
-    __syncthreads();
-    const double d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
-    S[L.D1B + i] = d1b;
-    __syncthreads();
-    z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
-    S[L.D1 + i] = d1 + d1b;
-    __syncthreads();
+    zz = isum<NP>(z * z);
+    if (__any(act && !(zz > 0.5 * nn2))) {
+        S[L.BC + i] = z;
+        __syncthreads();
+        const double d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
+        S[L.D1B + i] = d1b;
+        __syncthreads();
+        z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
+        S[L.D1 + i] = d1 + d1b;
+        zz = isum<NP>(z * z);
+        __syncthreads();
+    }
     return z;
 }
 
@@ -142,7 +153,9 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 // feasible (lambda >= 0 but on equality bounds); the loop then continues from it as from any of its
 // own states, else it starts cold. It changes the path, never the solution. With record set, the
 // final active set goes to ws_rows (status 0).
-template <int NP, int M0>
+// (LAPS: the diagnostic build's lap counters of this call go to stamp slots 20-27 / 13-14 -- the inline
+// call only: the repair kernel's own stamps use those slots)
+template <int NP, int M0, bool LAPS = false>
 __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u_i, int &status, int &iters,
                                            bool &infeasible, int wsg = 0, bool record = false)
@@ -212,9 +225,9 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             const double nj = on ? sa * Mr.get(pa) : 0.0;
             S[L.NV + i] = nj;
             __syncthreads();
-            const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
-            const double zzr = isum<NP>(zr * zr);
             const double npn = __shfl(nrm, pa, NP);
+            double zzr;
+            const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr);
             if (on && !(zzr > 1e-16 * npn * npn)) dep = true; // a dependent batch: start cold
             double rr2 = 0.0;
             if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
@@ -296,8 +309,8 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         S[L.NV + i] = npj;
         __syncthreads();
         WBQ_LAP(3);
-        const double z = project_out<NP>(S, L, npj, q, i);
-        const double zz = isum<NP>(z * z);
+        double zz;
+        const double z = project_out<NP>(S, L, npj, q, i, npn * npn, go, zz);
         WBQ_LAP(4);
         double ra = 0.0;
         if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
@@ -382,8 +395,9 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 const double nj = on ? sa * Mr.get(pa) : 0.0;
                 S[L.NV + i] = nj;
                 __syncthreads();
-                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i);
-                const double zzr = isum<NP>(zr * zr);
+                const double npa = __shfl(nrm, pa, NP);
+                double zzr;
+                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npa * npa, on, zzr);
                 double rr2 = 0.0;
                 if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
                 if (on) {
@@ -412,7 +426,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     }
     const double xf = Mr.dot(S + L.U, NP);
     WBQ_LAP(7);
-    WBQ_LAP_FLUSH(20, 13);
+    if constexpr (LAPS) WBQ_LAP_FLUSH(20, 13);
     return xf;
 }
 
@@ -1109,7 +1123,7 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             bool inf = false;
             const int wsg = (ga && warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
             WBQ_STAMP(18); // (diagnostic build: the inline dual active set starts)
-            const double x2 = gi_solve<NP, M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
+            const double x2 = gi_solve<NP, M0, true>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
                                                true);
             WBQ_STAMP(19);
             const bool rep = active && (inf || to_rep);

@@ -228,17 +228,24 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
 // mask would read stale partials of inactive lanes. Diagnostic builds (-DWBQ_STAMPS) check the
 // precondition at every reduction and report a violation (printf from the first active lane; no
 // trap: a fault can take the whole GPU down); the product build does not.
+// With NP = 32 a reduction reads only its own instance's half of the wave, so a mask that keeps each
+// half whole (an instance-uniform branch) is fine; NP = 64 (and the contact kernel's 64-lane
+// reductions) need every lane.
 #ifdef WBQ_STAMPS
-#define WBQ_FULL_EXEC()                                                                 \
+#define WBQ_FULL_EXEC_NP(NP_)                                                           \
     do {                                                                                \
         const unsigned long long ex_ = __builtin_amdgcn_read_exec();                    \
-        if (ex_ != ~0ull && (int)(threadIdx.x & 63) == __builtin_ctzll(ex_))             \
+        const unsigned lo_ = (unsigned)ex_, hi_ = (unsigned)(ex_ >> 32);                 \
+        const bool ok_ = (NP_) == 32 ? ((lo_ == 0u || lo_ == ~0u) && (hi_ == 0u || hi_ == ~0u)) \
+                                     : ex_ == ~0ull;                                    \
+        if (!ok_ && (int)(threadIdx.x & 63) == __builtin_ctzll(ex_))                     \
             printf("wbq: reduction under a lane mask (exec %llx) in block %d at %s:%d\n", \
                    ex_, (int)blockIdx.x, __FILE__, __LINE__);                            \
     } while (0)
 #else
-#define WBQ_FULL_EXEC() do {} while (0)
+#define WBQ_FULL_EXEC_NP(NP_) do {} while (0)
 #endif
+#define WBQ_FULL_EXEC() WBQ_FULL_EXEC_NP(64)
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
@@ -266,7 +273,7 @@ template <int NP>
 __device__ __forceinline__ double isum(double v)
 {
     static_assert(NP == 32 || NP == 64, "isum: NP");
-    WBQ_FULL_EXEC();
+    WBQ_FULL_EXEC_NP(NP);
     v += dpp_f64<kDppXor1>(v);
     v += dpp_f64<kDppXor2>(v);
     v += dpp_f64<kDppHalfMirror>(v);
@@ -280,7 +287,7 @@ template <int NP>
 __device__ __forceinline__ double imax(double v)
 {
     static_assert(NP == 32 || NP == 64, "imax: NP");
-    WBQ_FULL_EXEC();
+    WBQ_FULL_EXEC_NP(NP);
     v = fmax(v, dpp_f64<kDppXor1>(v));
     v = fmax(v, dpp_f64<kDppXor2>(v));
     v = fmax(v, dpp_f64<kDppHalfMirror>(v));
@@ -311,7 +318,7 @@ template <int NP, bool MAX>
 __device__ __forceinline__ void iarg(double &v, int &idx)
 {
     static_assert(NP == 32 || NP == 64, "iarg: NP");
-    WBQ_FULL_EXEC();
+    WBQ_FULL_EXEC_NP(NP);
     arg_stage<kDppXor1, MAX>(v, idx);
     arg_stage<kDppXor2, MAX>(v, idx);
     arg_stage<kDppHalfMirror, MAX>(v, idx);
@@ -345,7 +352,7 @@ template <int NP, int K>
 __device__ __forceinline__ void isum_vec(double (&v)[K])
 {
     static_assert(NP == 32 || NP == 64, "isum_vec: NP");
-    WBQ_FULL_EXEC();
+    WBQ_FULL_EXEC_NP(NP);
 #pragma unroll
     for (int c = 0; c < K; ++c) v[c] += dpp_f64<kDppXor1>(v[c]);
 #pragma unroll

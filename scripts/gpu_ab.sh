@@ -9,6 +9,9 @@ for lib in qppvm_amd/libwbq.so abv/*.so; do
   nm=$(basename "$lib" .so)
   timeout -k 10 200 python scripts/ab_bench.py "$lib" $ARGS1 ${EXTRA:-} > gpurun_out/ab_${nm}_c1.log 2>&1 || exit 1
   timeout -k 10 200 python scripts/ab_bench.py "$lib" $ARGS2 ${EXTRA:-} > gpurun_out/ab_${nm}_c2.log 2>&1 || exit 1
+  if [ -n "${C4:-}" ]; then
+    timeout -k 10 200 python scripts/ab_bench.py "$lib" --config 4 --steps 20 --warmup 3 --no-cpu --no-pmc --no-variant > gpurun_out/ab_${nm}_c4.log 2>&1 || exit 1
+  fi
   if [ -n "${W1M:-}" ]; then
     timeout -k 10 200 python scripts/ab_bench.py "$lib" $ARGS1 --weight M > gpurun_out/ab_${nm}_c1m.log 2>&1 || exit 1
   fi
@@ -16,7 +19,7 @@ for lib in qppvm_amd/libwbq.so abv/*.so; do
 import json, sys
 nm = sys.argv[1]
 import os
-for c in ("c1", "c2", "c1m"):
+for c in ("c1", "c2", "c4", "c1m"):
     if not os.path.exists(f"gpurun_out/ab_{nm}_{c}.log"): continue
     d = json.loads(open(f"gpurun_out/ab_{nm}_{c}.log").read().strip().splitlines()[-1])
     r = d.get("roofline", {})
