@@ -62,6 +62,11 @@
 #ifndef WBQ_FAST_EQ_EARLY
 #define WBQ_FAST_EQ_EARLY 0
 #endif
+// dual active set, n > 32 (T rows in LDS): a dropped bound leaves the basis by Givens rotations (1) or by
+// re-projecting the later active normals (0, rounds 1-4; always for n <= 32)
+#ifndef WBQ_GI_GIVENS
+#define WBQ_GI_GIVENS 1
+#endif
 
 namespace wbq {
 namespace {
@@ -153,15 +158,18 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 // feasible (lambda >= 0 but on equality bounds); the loop then continues from it as from any of its
 // own states, else it starts cold. It changes the path, never the solution. With record set, the
 // final active set goes to ws_rows (status 0).
-// (LAPS: the diagnostic build's lap counters of this call go to stamp slots 20-27 / 13-14 -- the inline
-// call only: the repair kernel's own stamps use those slots)
-template <int NP, int M0, bool LAPS = false>
+// (LAPB / LAPC: stamp slots of the diagnostic build's lap counters of this call site, 8 phases from LAPB
+// and 2 counts from LAPC; 0: none)
+template <int NP, int M0, int LAPB = 0, int LAPC = 0>
 __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u_i, int &status, int &iters,
-                                           bool &infeasible, int wsg = 0, bool record = false)
+                                           bool &infeasible, int wsg = 0, bool record = false, int handoff = 0)
 {
     constexpr int RS = NP + 1;
     constexpr bool MREG = ActiveLayout<NP>::MREG;
+    // (the Givens drop with T rows in LDS only: in the NP = 32 merged kernel, T in registers, its
+    // temporaries spilled the fast path, 0 -> 428 B)
+    constexpr bool kGivens = WBQ_GI_GIVENS != 0 && !MREG;
     const int n = a.n, m0 = a.m0;
     const ActiveLayout<NP> L(a.ntasks, m0);
     const int ic = i < n ? i : n - 1;
@@ -370,11 +378,72 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 status = 1;
                 go = false;
             }
+            // handoff > 0: a loop still running after that many steps goes to the level-0 repair as if
+            // infeasible (its BVLS settles level 0 first; a feasible instance comes back unpinned, so the
+            // result is the same)
+            if (handoff > 0 && iters >= handoff && go) {
+                infeasible = true;
+                go = false;
+            }
         }
         S[L.U + i] = u_i;
         __syncthreads();
         WBQ_LAP(5);
         if (__any(rebuild)) {
+          if constexpr (kGivens) {
+            // Drop slot c by a QR downdate. With the active normals N = Q^T R (Q: the basis rows m0.. of
+            // Q1T, R = T^-1), deleting column c of R leaves it upper Hessenberg from c; the plane rotations
+            // G_c .. G_{k-1} that restore the triangle are the ones that carry row c of T onto e_k
+            // (G^T e_k spans the left null space of R without column c, which is row c of T), so they are
+            // found from T alone by a chase down that row. Then Q <- G Q (its last row leaves the basis),
+            // T <- (T without row c) G^T (its last column drops out): two LDS rows and two entries per lane
+            // per rotation, where re-projecting every later normal cost two to four LDS dot products each
+            // (the stress plant's n = 39 dual loops spent ~60 % of their cycles there, scripts/diag_plugin_tick.py).
+            const int kold = k + 1; // (the drop above decremented k)
+            if (rebuild && i == cdrop) {
+#pragma unroll
+                for (int j = 0; j < NP; ++j) S[L.BC + j] = Tr.at(j); // row c of T, every lane reads it
+            }
+            __syncthreads();
+            double xr = rebuild ? S[L.BC + cdrop] : 0.0; // the chase's running entry
+#pragma unroll
+            for (int j = 0; j + 1 < NP; ++j) {
+                const bool on = rebuild && j >= cdrop && j + 1 < kold;
+                if (__any(on)) {
+                    const double xn = S[L.BC + j + 1];
+                    const double h = sqrt(fma(xr, xr, xn * xn));
+                    const double ih = h > 0.0 ? 1.0 / h : 0.0;
+                    const double cs = h > 0.0 ? xn * ih : 1.0, sn = h > 0.0 ? -xr * ih : 0.0;
+                    if (on) {
+                        const double t0 = Tr.at(j), t1 = Tr.at(j + 1);
+                        Tr.set(j, fma(cs, t0, sn * t1));
+                        Tr.set(j + 1, fma(-sn, t0, cs * t1));
+                        double *q0 = S + L.QA + (m0 + j) * RS + i;
+                        const double a0 = q0[0], a1 = q0[RS];
+                        q0[0] = fma(cs, a0, sn * a1);
+                        q0[RS] = fma(-sn, a0, cs * a1);
+                        xr = h;
+                    }
+                }
+            }
+            // rows c.. of T move up one slot (the multipliers and slot rows did above)
+            const int nxt = i + 1 < NP ? i + 1 : i;
+            {
+                double nrow[NP];
+#pragma unroll
+                for (int j = 0; j < NP; ++j) nrow[j] = __shfl(Tr.at(j), nxt, NP);
+                __syncthreads(); // (T rows in LDS: every read of row i + 1 before its owner writes it)
+#pragma unroll
+                for (int j = 0; j < NP; ++j) {
+                    double v = (rebuild && i >= cdrop) ? nrow[j] : Tr.at(j);
+                    if (rebuild && (j >= k || i >= k)) v = 0.0; // the last column and the dead rows
+                    if (rebuild) Tr.set(j, v);
+                }
+            }
+            if (rebuild) q = m0 + k;
+            __syncthreads();
+            WBQ_LAP_ADD(1, 1);
+          } else {
             // Re-factor the inequality directions from the dropped position on: Q1T rows
             // m0+cdrop.. and T columns cdrop.. (Gram-Schmidt is sequential, earlier ones stand).
             if (rebuild) {
@@ -410,6 +479,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 __syncthreads();
                 WBQ_LAP_ADD(1, 1);
             }
+          }
             WBQ_LAP(6);
         }
     }
@@ -426,14 +496,16 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     }
     const double xf = Mr.dot(S + L.U, NP);
     WBQ_LAP(7);
-    if constexpr (LAPS) WBQ_LAP_FLUSH(20, 13);
+    if constexpr (LAPB > 0) WBQ_LAP_FLUSH(LAPB, LAPC);
     return xf;
 }
 
 // Active-set kernel (NP = 64; NP = 32 runs it inline in the fast kernel): instances parked
 // with status -1. An instance whose active set finds level 0 infeasible is handed on to the
 // repair kernel with status -2.
-template <int NP, int M0>
+// PIN (NP = 64): the hand-back pass after the repair kernel -- work list 2, the instances' pinned limits
+// from lo_scr / hi_scr, warm from the BVLS bound set; "no step" there is status 2, as in the repair kernel.
+template <int NP, int M0, bool PIN = false>
 __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(const QppvmArgs a)
 {
     constexpr int IPW = kWave / NP;
@@ -443,18 +515,25 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
-    const int cnt = a.work[a.epoch * 2]; // instances parked in this solve
+    const int cnt = PIN ? a.work[4 + a.epoch] : a.work[a.epoch * 2]; // instances parked in this solve
     for (long e0 = (long)blockIdx.x * IPW; e0 < cnt; e0 += (long)gridDim.x * IPW) {
         const long e = e0 + sub;
         const bool valid = e < cnt;
         WBQ_STAMP(4);
         WBQ_RTSTAMP(30);
-        const long b = valid ? a.wl[e] : 0;
+        const long b = valid ? a.wl[(PIN ? 2 * a.B : 0) + e] : 0;
         const int n = a.n;
         const bool row = valid && i < n;
         const double h_i = row ? a.h[b * n + i] : 0.0;
         double lo = -kInf, hi = kInf;
-        if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
+        if constexpr (PIN) {
+            if (row) {
+                lo = a.lo_scr[b * NP + i];
+                hi = a.hi_scr[b * NP + i];
+            }
+        } else {
+            if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
+        }
         const double *qs = a.q1_scr + b * kM0Max * NP;
         __syncthreads(); // the previous instance's LDS is dead
 #pragma unroll
@@ -463,11 +542,25 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         int status = 0, iters = 0;
         bool infeasible = false;
         WBQ_STAMP(6);
-        const bool warm_gi = valid && (a.ws_hint[b] & 2);
+        const bool warm_gi = valid && (PIN || (a.ws_hint[b] & 2));
         const int wsg = (warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
-        const double x_i = gi_solve<NP, M0>(a, S, b, i, row, valid, lo, hi, valid ? a.u_scr[b * NP + i] : 0.0,
-                                            status, iters, infeasible, wsg, true);
-        if (infeasible) {
+        const double x_i = gi_solve<NP, M0, PIN ? 48 : 32, PIN ? 56 : 40>(a, S, b, i, row, valid, lo, hi,
+                                                                        valid ? a.u_scr[b * NP + i] : 0.0, status,
+                                                                        iters, infeasible, wsg, true,
+                                                                        PIN ? 0 : a.gi_handoff);
+        if constexpr (PIN) { // (the repair kernel's epilogue)
+            if (infeasible && status == 0) status = 2;
+            double tau_i = x_i + h_i;
+            if (imax<NP>((row && !isfinite(tau_i)) ? 1.0 : 0.0) > 0.0 && status == 0) status = 3;
+            if (status != 0) tau_i = h_i;
+            if (row) a.tau[b * n + i] = tau_i;
+            rollout_step(a, b, i, row, S[L.U + i], status == 0);
+            if (valid && i == 0) {
+                a.status[b] = status;
+                a.iters[b] += iters;
+                a.ws_hint[b] = (a.ws_hint[b] & 1) | (status == 0 ? 2 : 0);
+            }
+        } else if (infeasible) {
             if (valid && i == 0) {
                 a.status[b] = -2; // level-0 repair kernel
                 wl_push(a, 1, b);
@@ -531,8 +624,31 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     // level-1 optimum keeps level 0 at y*, so its active bounds are mostly those BVLS ended on: a config-4
     // rollout's repaired instance-steps took up to ~90 cold steps (scripts/diag_mpc_steps.py)
     const int wsr = (row && !uniq) ? -ro.st : 0; // gi_solve's sides: +1 lower, -1 upper
+    if constexpr (NP == 64) {
+        // hand the pinned level 1 to the active-set pass over work list 2 (qppvm_active_kernel<..., true>):
+        // the dual loop there runs ~2x faster per step than here, where it shares the BVLS's frame
+        // (scripts/diag_plugin_tick.py, stress plant: ~39k vs ~19k cycles per step)
+        if (a.handback && rep && ro.status == 0 && !uniq) { // (one instance per wave: wave-uniform)
+            if (row) {
+                a.lo_scr[b * NP + i] = ro.lo;
+                a.hi_scr[b * NP + i] = ro.hi;
+            }
+            a.u_scr[b * NP + i] = ro.u;
+#pragma unroll
+            for (int c = 0; c < M0; ++c)
+                if (c < a.m0) a.q1_scr[(b * kM0Max + c) * NP + i] = S[L.QA + c * (NP + 1) + i];
+            a.ws_rows[b * 64 + i] = (signed char)(row ? wsr : 0);
+            if (i == 0) {
+                a.status[b] = -1;
+                a.iters[b] = ro.it;
+                a.ws_hint[b] = ro.l0inf ? 1 : 0;
+                wl_push(a, 2, b);
+            }
+            return;
+        }
+    }
     if (__any(rep && !uniq))
-        x_i = gi_solve<NP, M0>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
+        x_i = gi_solve<NP, M0, 48, 56>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
                                infeasible, wsr, true);
     if (uniq) x_i = ro.x;
     if (a.integrate && __any(rep && uniq)) { // rollouts integrate qdd = u = M^-1 x*
@@ -607,6 +723,7 @@ __global__ __launch_bounds__(64, 1) void qppvm_repair_kernel(const QppvmArgs a)
     if (blockIdx.x == 0 && threadIdx.x == 0) { // the next solve's counters (its parity was last
         a.work[(a.epoch ^ 1) * 2] = 0;         // used by the previous solve, which has completed)
         a.work[(a.epoch ^ 1) * 2 + 1] = 0;
+        if (a.handback) a.work[4 + (a.epoch ^ 1)] = 0; // (the hand-back pass runs after this kernel)
     }
     follow_publish(a.fg, a.work[a.epoch * 2], cnt);
     if ((long)blockIdx.x * IPW >= cnt) return;
@@ -1123,7 +1240,7 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             bool inf = false;
             const int wsg = (ga && warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
             WBQ_STAMP(18); // (diagnostic build: the inline dual active set starts)
-            const double x2 = gi_solve<NP, M0, true>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
+            const double x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
                                                true);
             WBQ_STAMP(19);
             const bool rep = active && (inf || to_rep);
@@ -1213,8 +1330,18 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 // fast kernel; without the per-step launch boundary an instance whose repair runs long delays only its
 // own wave instead of every instance's next step (config 4 with per-step launches: the rare repaired
 // instance-steps, ~0.3 %, held whole launches for hundreds of microseconds).
+// (WBQ_ROLL_W: waves per SIMD of the fused rollout, 2 as the fast kernel; 1 gives its dual active-set loop
+// 512 registers -- no spills, LDS reads in flight -- at half the resident instances)
+#ifndef WBQ_ROLL_W
+#define WBQ_ROLL_W 2
+#endif
+// (diagnostic: WBQ_ROLL_ARG=a hands the steps the by-value kernel argument itself instead of the laundered
+// kernarg-segment reference -- with WBQ_ROLL_REPAIR_NOINLINE, round 4's faulting build)
+#ifndef WBQ_ROLL_ARG
+#define WBQ_ROLL_ARG as
+#endif
 template <int NP, int M0, int TM>
-__global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
+__global__ __launch_bounds__(64, WBQ_ROLL_W) void qppvm_rollout_kernel(const QppvmArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x == 0) { // one launch: the next solve's counters (as INLREP)
         a.work[(a.epoch ^ 1) * 2] = 0;
@@ -1230,7 +1357,7 @@ __global__ __launch_bounds__(64, 2) void qppvm_rollout_kernel(const QppvmArgs a)
         KPtr kp = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(kp));
         const QppvmArgs &as = *(const QppvmArgs *)(const char *)kp;
-        fast_body<NP, M0, true, TM, 2, 32, true, true>(as);
+        fast_body<NP, M0, true, TM, WBQ_ROLL_W, 32, true, true>(WBQ_ROLL_ARG);
         __syncthreads(); // this wave's q, qd and warm-start writes are visible to its next step
     }
     WBQ_STAMP(29);
@@ -1314,7 +1441,10 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
         const unsigned g0 = follow_blocks(a.fg.est[0], IPW, kFollowGrid, a.B);
         e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, g0, stream);
         if (e != hipSuccess) return e;
-        return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
+        e = launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
+        if (e != hipSuccess || !(a.handback || a.prepare)) return e;
+        // the repaired instances' dual active sets (work list 2), sized like the repair grid
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0, true>, a, g1, stream);
     }
 }
 

@@ -1150,7 +1150,7 @@ __device__ __forceinline__ RepairOut level0_repair(const QppvmArgs &a, int soff,
 // broadcast load per block of at most kFollowGrid blocks, instead of a batch-sized grid.
 __device__ __forceinline__ void wl_push(const QppvmArgs &a, int list, long b)
 {
-    const int idx = atomicAdd(&a.work[a.epoch * 2 + list], 1);
+    const int idx = atomicAdd(&a.work[list < 2 ? a.epoch * 2 + list : 4 + a.epoch], 1);
     a.wl[(long)list * a.B + idx] = (int)b;
     // (the host's completion check of an on-demand solve: some instance waits for the repair kernel)
     if (list == 1 && a.self_book && a.fg.seen)

@@ -74,6 +74,7 @@ struct wbq_ctx {
     unsigned long long *stamps = nullptr; // diagnostic builds only
     double *u_scr = nullptr, *q1_scr = nullptr; // fast -> active-set hand-off
     double *ui_scr = nullptr, *b0_scr = nullptr; // u_imp and b0 for the level-0 repair
+    double *lo_scr = nullptr, *hi_scr = nullptr; // n > 32: repair -> active-set hand-back (pinned limits)
     int *work = nullptr; // [2][2] per-solve work counters (see wbq_kernels.h)
     int *wl = nullptr;   // [2][max_batch] work lists
     unsigned char *ws_hint = nullptr; // [B] warm start (see wbq_kernels.h)
@@ -87,6 +88,8 @@ struct wbq_ctx {
     int opt_inline = env_option("WBQ_INLREP", -1); // WBQ_OPT_INLINE_REPAIR
     int opt_fused = env_option("WBQ_FUSED_ROLLOUT", 1); // WBQ_OPT_FUSED_ROLLOUT
     int opt_followup = env_option("WBQ_FOLLOWUP", 1);  // WBQ_OPT_FOLLOWUP
+    int opt_handback = env_option("WBQ_HANDBACK", 1);  // n > 32: repaired instances' dual loop in the active pass
+    int opt_handoff = env_option("WBQ_GI_HANDOFF", 0);  // n > 32: active-set steps before the repair takes over
     // on-demand follow-up: the last solve skipped its repair kernel; completed when outputs are read
     bool pending = false;
     wbq::QppvmArgs pend_args{};
@@ -378,10 +381,12 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
              hipMalloc(&c->q1_scr, B * wbq::kM0Max * np * 8) == hipSuccess &&
              hipMalloc(&c->ui_scr, B * np * 8) == hipSuccess &&
              hipMalloc(&c->b0_scr, B * wbq::kM0Max * 8) == hipSuccess &&
-             hipMalloc(&c->work, 4 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 4 * sizeof(int)) == hipSuccess &&
-             alloc_work_seen(c) && hipMalloc(&c->wl, 2 * B * sizeof(int)) == hipSuccess &&
+             hipMalloc(&c->work, 6 * sizeof(int)) == hipSuccess && hipMemset(c->work, 0, 6 * sizeof(int)) == hipSuccess &&
+             alloc_work_seen(c) && hipMalloc(&c->wl, 3 * B * sizeof(int)) == hipSuccess &&
              hipMalloc(&c->ws_hint, B) == hipSuccess && hipMemset(c->ws_hint, 0, B) == hipSuccess &&
              hipMalloc(&c->ws_state, B * np) == hipSuccess && hipMemset(c->ws_state, 0, B * np) == hipSuccess;
+        if (ok && np == 64 && !cspace) // (the hand-back of repaired instances, one per wave)
+            ok = hipMalloc(&c->lo_scr, B * np * 8) == hipSuccess && hipMalloc(&c->hi_scr, B * np * 8) == hipSuccess;
         if (ok) // the active sets' warm start (W1 = M: dual_gi.h; W1 = I: qppvm_kernel.hip gi_solve)
             ok = hipMalloc(&c->ws_rows, B * 64) == hipSuccess && hipMemset(c->ws_rows, 0, B * 64) == hipSuccess;
         c->np = np;
@@ -625,6 +630,10 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.u_scr = c->u_scr;
     a.q1_scr = c->q1_scr;
     a.ui_scr = c->ui_scr;
+    a.lo_scr = c->lo_scr;
+    a.hi_scr = c->hi_scr;
+    a.handback = (c->lo_scr && c->opt_handback) ? 1 : 0;
+    a.gi_handoff = a.handback ? c->opt_handoff : 0;
     a.b0_scr = c->b0_scr;
     a.work = c->work;
     a.wl = c->wl;
@@ -993,6 +1002,8 @@ void wbq_destroy(wbq_ctx *c)
     if (c->u_scr) (void)hipFree(c->u_scr);
     if (c->q1_scr) (void)hipFree(c->q1_scr);
     if (c->ui_scr) (void)hipFree(c->ui_scr);
+    if (c->lo_scr) (void)hipFree(c->lo_scr);
+    if (c->hi_scr) (void)hipFree(c->hi_scr);
     if (c->b0_scr) (void)hipFree(c->b0_scr);
     if (c->work) (void)hipFree(c->work);
     if (c->work_seen) (void)hipHostFree(c->work_seen);

@@ -225,13 +225,14 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
 // broke every contact-form variant whose dual loop reduces under a lane mask -- the swap moves active
 // lanes only -- while v_readlane reads the row's partial whatever the mask.)
 // The reductions read the four row partials with v_readlane whatever EXEC holds: a call under a lane
-// mask would read stale partials of inactive lanes. Diagnostic builds (-DWBQ_STAMPS) check the
+// mask would read stale partials of inactive lanes. Builds with -DWBQ_EXEC_CHECK check the
 // precondition at every reduction and report a violation (printf from the first active lane; no
-// trap: a fault can take the whole GPU down); the product build does not.
+// trap: a fault can take the whole GPU down); the product build does not. (Not part of the stamp build:
+// the printf at every reduction made a stamped qppvm unit take ~25 min to compile.)
 // With NP = 32 a reduction reads only its own instance's half of the wave, so a mask that keeps each
 // half whole (an instance-uniform branch) is fine; NP = 64 (and the contact kernel's 64-lane
 // reductions) need every lane.
-#ifdef WBQ_STAMPS
+#ifdef WBQ_EXEC_CHECK
 #define WBQ_FULL_EXEC_NP(NP_)                                                           \
     do {                                                                                \
         const unsigned long long ex_ = __builtin_amdgcn_read_exec();                    \

@@ -75,8 +75,16 @@ struct QppvmArgs {
     // instances parked for the active-set kernel (listed in wl[0, B)), [+1] those for the
     // repair kernel (wl[B, 2B)). The follow-up kernels run small grid-stride grids over the
     // lists; the repair kernel (the last launch) clears the other parity's counters.
-    int *work;       // [2][2] counters: instances appended to the two work lists this solve
-    int *wl;         // [2][B] work lists: [0, B) active-set kernel, [B, 2B) repair kernel
+    int *work;       // [2][2] counters: instances appended to the two work lists this solve; [4 + epoch]: list 2
+    int *wl;         // [3][B] work lists: [0, B) active-set kernel, [B, 2B) repair kernel, [2B, 3B) hand-back
+    // NP = 64: the repair kernel hands an instance whose pinned level 1 needs the dual active set back to
+    // an active-set pass over work list 2 (its pinned limits in lo_scr / hi_scr, u and Q1 in u_scr /
+    // q1_scr, the BVLS bound set in ws_rows) instead of running the loop inside its own large frame
+    double *lo_scr, *hi_scr; // [B][NP]
+    int handback;
+    // > 0 (NP = 64 active-set pass): a dual loop still running after that many steps is handed to the
+    // level-0 repair (a loop that long mostly ends "level 0 infeasible" after all)
+    int gi_handoff;
     int epoch;       // 0 / 1
     FollowGrid fg;   // follow-up grid sizing (see FollowGrid)
     // per-instance warm start across solves (the qpOASES hot-start analogue; it changes the
@@ -130,7 +138,9 @@ __device__ __forceinline__ void torque_box(const QppvmArgs &a, int j, double q, 
     hi = u - h;
 }
 
-constexpr int kStamps = 32; // fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7 (+30,31); repair 8-12 (+28,29); BVLS split 20-27
+// fast 0-3,5,15 (+16,17 realtime); active-set 4,6,7 (+30,31); repair 8-12 (+28,29); BVLS split 20-27;
+// dual-loop lap counters (gi_solve): inline 20-27 / 13-14, active kernel 32-39 / 40-41, repair 48-55 / 56-57
+constexpr int kStamps = 64;
 
 // Raise a kernel's dynamic-LDS limit on the current device to at least `bytes` (once per
 // device and kernel; thread-safe: contexts on several devices or threads share it). Called only

@@ -26,7 +26,7 @@ def run(prob, inp, reps=10):
         s.solve()
     ms, km, cnt = s.get_timing_detail()
     B = inp["h"].shape[0]
-    K = 32
+    K = 64
     buf = (ctypes.c_ulonglong * (K * B))()
     s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     assert s.lib.wbq_diag_stamps(s.ctx, buf, B) == 0

@@ -1,7 +1,7 @@
 """Diagnostics (GPU box, stamp build): where the dual active set's time goes (gi_solve's lap
 counters, qppvm_kernel.hip) in a config-2 churned solve and a config-4 fused rollout.
 
-Slots per block (kStamps = 32): 20-27 cycles summed per gi_solve phase (0 setup / M rows, 1 warm batch
+Slots per block (kStamps = 64): 20-27 cycles summed per gi_solve phase (0 setup / M rows, 1 warm batch
 projections, 2 warm step, 3 select, 4 project_out + |z|^2, 5 step + add/drop, 6 rebuild after a drop,
 7 record + final x), 13 loop passes, 14 rebuild projections, 6 / 7 inline repairs' cycles and count,
 28-29 / 30-31 the fused rollout's whole-block shader / realtime clocks."""
@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from qppvm_amd import wbq  # noqa: E402
 
-K = 32
+K = 64
 LAPS = ["setup", "warm_batch", "warm_step", "select", "project_out", "step_add_drop", "rebuild", "record"]
 
 

@@ -30,7 +30,7 @@ def run(libpath, prob, inp, reps=20, stamps=False):
     if stamps:
         B = inp["h"].shape[0]
         nb = B if prob.n > 32 else (B + 1) // 2  # blocks of the fast kernel: 2 instances per wave for n <= 32
-        K = 32
+        K = 64
         buf = (ctypes.c_ulonglong * (K * nb))()
         s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         assert s.lib.wbq_diag_stamps(s.ctx, buf, nb) == 0

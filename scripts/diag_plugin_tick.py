@@ -34,7 +34,8 @@ def main():
     wbq.load_library(lib)
     s = wbq.QPPVMSolver(prob, max_batch=1)
     s.lib.wbq_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    K = 32
+    s.lib.wbq_diag_stamps_clear.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    K = 64
     rows = []
     for t in range(ticks):
         inp = {k: np.ascontiguousarray(d[k][t:t + 1]) for k in ("M", "J", "pose", "pose_ref", "q", "qd", "qref", "h")}
@@ -42,6 +43,7 @@ def main():
         inp["pose_ref"] = inp["pose_ref"].reshape(1, 2, 12)
         s.set_inputs(inp)
         s.sync()
+        s.lib.wbq_diag_stamps_clear(s.ctx, 1)  # (the dual loops' lap counters add up)
         s.set_timing(True)
         s.solve()
         s.sync()
@@ -66,6 +68,14 @@ def main():
             row["rt_us"]["span"] = (st[29] - t0) / 100.0
             row["repair_clock_ghz"] = (st[12] - st[8]) / max(1.0, (st[29] - st[28]) / 100.0) / 1e3
         row["fast_clock_ghz"] = (st[5] - st[0]) / max(1.0, (st[17] - st[16]) / 100.0) / 1e3
+        # the dual loop's lap counters (gi_solve): active-set kernel slots 32-41, repair kernel 48-57
+        for nm, base, cb in (("active_gi", 32, 40), ("repair_gi", 48, 56)):
+            laps = [int(v) for v in st[base:base + 8]]
+            if sum(laps) > 0:
+                passes = int(st[cb])
+                row[nm] = {"cycles": sum(laps), "passes": passes, "rebuild_proj": int(st[cb + 1]),
+                           "cycles_per_pass": (laps[3] + laps[4] + laps[5]) / max(passes, 1),
+                           "laps_setup_warm_wstep_select_proj_step_rebuild_rec": laps}
         if rep:
             row.update({"gj": int(st[9] - st[8]), "bvls": int(st[10] - st[9]), "pins_eq": int(st[11] - st[10]),
                         "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14]),

@@ -1,0 +1,80 @@
+"""n > 32: the repair kernel hands an instance whose pinned level 1 needs the dual active set back to an
+active-set pass over work list 2 (qppvm_kernel.hip, qppvm_active_kernel<..., true>) instead of running the
+loop itself. Same results as the in-repair loop (WBQ_HANDBACK=0, read when a context is created) and as
+the oracle (tau within 1e-6 relative, statuses equal), cold and warm, and in per-step rollouts."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from qppvm_amd.problem import QPPVMProblem
+from qppvm_amd.synth import qppvm_instances
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def wbq_mod():
+    from qppvm_amd import build, wbq
+    build.build()
+    return wbq
+
+
+def solver(wbq_mod, prob, B, handback):
+    old = os.environ.get("WBQ_HANDBACK")
+    os.environ["WBQ_HANDBACK"] = "1" if handback else "0"
+    try:
+        return wbq_mod.QPPVMSolver(prob, max_batch=B)
+    finally:
+        if old is None:
+            del os.environ["WBQ_HANDBACK"]
+        else:
+            os.environ["WBQ_HANDBACK"] = old
+
+
+@pytest.mark.parametrize("n,tm", [(39, 30.0), (39, 80.0), (48, 40.0)])
+def test_handback_matches_in_repair_loop_and_oracle(wbq_mod, oracle_lib, n, tm):
+    prob = QPPVMProblem(n=n, tau_max=tm)
+    inp = qppvm_instances(prob, 96, seed=900 + n + int(tm))
+    out = {}
+    for hb in (0, 1):
+        s = solver(wbq_mod, prob, 96, hb)
+        try:
+            first = s.solve_batch(inp)
+            warm = s.solve_batch(inp)  # warm: repair hints and bound sets from the first solve
+        finally:
+            s.close()
+        out[hb] = (first, warm)
+    tau_o, st_o, _ = oracle_lib.qppvm_batch(prob, inp)
+    for hb in (0, 1):
+        for tau, st, _ in out[hb]:
+            np.testing.assert_array_equal(st, st_o)
+            ok = st_o == 0
+            assert rel_err(tau[ok], tau_o[ok]) <= TOL
+    # the two paths run the same loop on the same data
+    for k in range(2):
+        np.testing.assert_array_equal(out[0][k][1], out[1][k][1])
+        assert rel_err(out[1][k][0], out[0][k][0]) <= 1e-9
+
+
+def test_handback_per_step_rollout(wbq_mod):
+    """n = 39 rollouts run per-step launches (fast, active, repair, hand-back pass): the integrated
+    state is the same with and without the hand-back."""
+    prob = QPPVMProblem(n=39, tau_max=40.0)
+    inp = qppvm_instances(prob, 32, seed=977, plant=True)
+    res = []
+    for hb in (0, 1):
+        s = solver(wbq_mod, prob, 32, hb)
+        try:
+            s.set_inputs(inp)
+            s.rollout(6, 1e-3)
+            tau, st, _ = s.outputs()
+            q, qd = s.state()
+        finally:
+            s.close()
+        res.append((tau, st, q, qd))
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][2:], res[1][2:]):
+        assert np.abs(a - b).max() <= 1e-9 * max(1.0, np.abs(a).max())
