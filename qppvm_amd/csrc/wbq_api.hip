@@ -89,7 +89,9 @@ struct wbq_ctx {
     int opt_fused = env_option("WBQ_FUSED_ROLLOUT", 1); // WBQ_OPT_FUSED_ROLLOUT
     int opt_followup = env_option("WBQ_FOLLOWUP", 1);  // WBQ_OPT_FOLLOWUP
     int opt_handback = env_option("WBQ_HANDBACK", 1);  // n > 32: repaired instances' dual loop in the active pass
-    int opt_handoff = env_option("WBQ_GI_HANDOFF", 0);  // n > 32: active-set steps before the repair takes over
+    // n > 32: active-set steps before the repair takes over (stress plant p99 1.17 -> 1.06 ms at 16-32 steps,
+    // profiles/r05_v6_dummy_stress_handoff.log; 0: never)
+    int opt_handoff = env_option("WBQ_GI_HANDOFF", 24);
     // on-demand follow-up: the last solve skipped its repair kernel; completed when outputs are read
     bool pending = false;
     wbq::QppvmArgs pend_args{};
