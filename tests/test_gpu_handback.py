@@ -78,3 +78,29 @@ def test_handback_per_step_rollout(wbq_mod):
     np.testing.assert_array_equal(res[0][1], res[1][1])
     for a, b in zip(res[0][2:], res[1][2:]):
         assert np.abs(a - b).max() <= 1e-9 * max(1.0, np.abs(a).max())
+
+
+@pytest.mark.parametrize("handoff", [1, 3])
+def test_active_loop_handoff_to_repair(wbq_mod, oracle_lib, handoff):
+    """WBQ_GI_HANDOFF (n > 32): an active-set loop still running after `handoff` steps goes to the level-0
+    repair as if infeasible; a feasible instance comes back with no pins, so the result is the oracle's."""
+    prob = QPPVMProblem(n=39, tau_max=60.0)
+    inp = qppvm_instances(prob, 64, seed=1234)
+    old = os.environ.get("WBQ_GI_HANDOFF")
+    os.environ["WBQ_GI_HANDOFF"] = str(handoff)
+    try:
+        s = wbq_mod.QPPVMSolver(prob, max_batch=64)
+    finally:
+        if old is None:
+            del os.environ["WBQ_GI_HANDOFF"]
+        else:
+            os.environ["WBQ_GI_HANDOFF"] = old
+    try:
+        tau, st, it = s.solve_batch(inp)
+    finally:
+        s.close()
+    tau_o, st_o, _ = oracle_lib.qppvm_batch(prob, inp)
+    np.testing.assert_array_equal(st, st_o)
+    ok = st_o == 0
+    assert rel_err(tau[ok], tau_o[ok]) <= TOL
+    assert (it > handoff).any()  # some instance did go the long way
