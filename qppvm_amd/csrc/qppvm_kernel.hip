@@ -686,8 +686,13 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 // overhead of any follow-up kernel (scripts/launch_probe2.hip, launch_probe3.hip: registers, LDS,
 // scratch, kernarg size and a cold L2 do not change it); rocprofv3's ~5 us duration for it includes
 // the dispatch.
-// (diagnostic: WBQ_ROLL_REPAIR_NOINLINE puts the fused rollout's inline repair behind a call -- the
-// round-4 variant that faulted on MI355X)
+// The fused rollout's level-0 repair behind a call (WBQ_ROLL_REPAIR_NOINLINE, default 1 since round 5): the
+// step's fast path then keeps its registers instead of spilling around the repair's (config 4, same box:
+// WRITE_SIZE per 20-step launch 730 -> 156 MB, a repair-free 4096 x 20 rollout 0.75 -> 0.51 ms, a repairing one
+// 3.25 -> 3.33 ms). Round 4's build of this faulted on MI355X; on round 5's sources it passes.
+#ifndef WBQ_ROLL_REPAIR_NOINLINE
+#define WBQ_ROLL_REPAIR_NOINLINE 1
+#endif
 template <int NP, int M0>
 __device__ __noinline__ void repair_instance_call(const QppvmArgs &a, double *S, long b, int i, bool rep)
 {
@@ -1299,11 +1304,10 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
 #ifdef WBQ_STAMPS
             const unsigned long long rt0_ = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef WBQ_ROLL_REPAIR_NOINLINE
-            if constexpr (ROLL) repair_instance_call<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
+            if constexpr (ROLL && WBQ_ROLL_REPAIR_NOINLINE != 0)
+                repair_instance_call<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
             else
-#endif
-            repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
+                repair_instance<NP, M0>(a, S, rep_inl ? b : 0, i, rep_inl);
 #ifdef WBQ_STAMPS
             // (diagnostic: inline repairs' cycles and count summed in slots 6 / 7)
             const unsigned long long rt1_ = __builtin_amdgcn_s_memtime();
@@ -1336,7 +1340,7 @@ __global__ __launch_bounds__(64, W) void qppvm_fast_kernel(const QppvmArgs a)
 #define WBQ_ROLL_W 2
 #endif
 // (diagnostic: WBQ_ROLL_ARG=a hands the steps the by-value kernel argument itself instead of the laundered
-// kernarg-segment reference -- with WBQ_ROLL_REPAIR_NOINLINE, round 4's faulting build)
+// kernarg-segment reference -- with the repair call, round 4's faulting build)
 #ifndef WBQ_ROLL_ARG
 #define WBQ_ROLL_ARG as
 #endif
