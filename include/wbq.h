@@ -180,10 +180,17 @@ typedef struct {
 
 int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out);
 int wbq_create_contact(const wbq_contact_desc *desc, int device, wbq_ctx **out);
-/* Launch on a caller-provided hipStream_t (NULL = the context's own stream). Solves of one
- * context must stay stream-ordered: switch streams only between a completed solve and the next
- * (a pending host-input copy made on the old stream is waited for). */
+/* Launch on a caller-provided hipStream_t (NULL = the context's own stream, created non-blocking;
+ * WBQ_NULL_STREAM = the device's legacy default stream, hipStream_t 0 -- e.g. torch's default stream,
+ * whose handle is 0 and so cannot be passed as itself). Solves of one context must stay stream-ordered:
+ * switch streams only between a completed solve and the next (a pending host-input copy made on the old
+ * stream is waited for). */
+#define WBQ_NULL_STREAM ((void *)1)
 int wbq_set_stream(wbq_ctx *ctx, void *hip_stream);
+/* WBQ_MEM_HOST inputs are copied into the context (pinned staging, one H2D copy on the stream);
+ * WBQ_MEM_DEVICE inputs are adopted in place: the caller keeps them alive and unchanged until the
+ * solves that read them have completed in stream order (with WBQ_MEM_DEVICE inputs every solve
+ * enqueues all of its kernels, so a refill enqueued on the stream after wbq_solve is safe). */
 int wbq_set_inputs(wbq_ctx *ctx, const wbq_inputs *in);
 int wbq_set_contact_inputs(wbq_ctx *ctx, const wbq_contact_inputs *in);
 int wbq_solve(wbq_ctx *ctx);
@@ -208,7 +215,9 @@ int wbq_get_contact_outputs(wbq_ctx *ctx, double *x);
 /* Write outputs into caller-owned device buffers ([batch][n] / [batch]) instead of the
  * context's (any NULL pointer reverts that output to the context buffer). */
 int wbq_set_outputs(wbq_ctx *ctx, double *tau, int32_t *status, int32_t *iters);
-/* Device-resident outputs of the last solve (valid until the next wbq_solve/destroy). */
+/* Device-resident outputs of the last solve: final when this call returns (a solve left pending by the
+ * on-demand follow-up, WBQ_OPT_FOLLOWUP, is completed first) and valid until the next wbq_solve /
+ * wbq_rollout / wbq_destroy. */
 int wbq_get_device_outputs(wbq_ctx *ctx, const double **tau, const int32_t **status,
                            const int32_t **iters);
 /* Drop the warm-start working set of instances with mask[b] != 0, b < the current batch (the
@@ -242,10 +251,20 @@ int wbq_get_timing_detail(wbq_ctx *ctx, double *solve_ms, double *kernel_ms, int
  *                           outputs: wbq_sync, wbq_get_outputs, wbq_get_device_outputs, wbq_get_state,
  *                           wbq_get_warmstart_hints (a later wbq_solve supersedes it). Not applied with
  *                           caller-owned device outputs (wbq_set_outputs: a stream consumer reads them
- *                           without a call), rollouts or the constraint-space stacks. 0: every solve enqueues
- *                           its follow-up kernel, so its outputs are final in stream order.
- *                           (env WBQ_FOLLOWUP) */
+ *                           without a call), WBQ_MEM_DEVICE inputs (the deferred repair would read the
+ *                           caller's buffers when the outputs are read, after the caller may have refilled
+ *                           them), rollouts or the constraint-space stacks. 0: every solve enqueues its
+ *                           follow-up kernel, so its outputs are final in stream order. (env WBQ_FOLLOWUP)
+ *   WBQ_OPT_HANDBACK        QPPVM W1 = I, n > 32: 1 (default) a repaired instance's pinned level-1 dual loop runs
+ *                           in a third launch (the active-set kernel over work list 2); 0 inside the repair
+ *                           kernel. (env WBQ_HANDBACK)
+ *   WBQ_OPT_GI_HANDOFF      QPPVM W1 = I, n > 32: a dual loop of the active-set kernel still running after this
+ *                           many steps (>= 0; default 24, 0 = never) is handed to the level-0 repair, which
+ *                           settles level 0 first (same result). Takes effect with WBQ_OPT_HANDBACK = 1.
+ *                           (env WBQ_GI_HANDOFF) */
 #define WBQ_OPT_FOLLOWUP 3
+#define WBQ_OPT_HANDBACK 4
+#define WBQ_OPT_GI_HANDOFF 5
 int wbq_set_option(wbq_ctx *ctx, int option, int value);
 void wbq_destroy(wbq_ctx *ctx);
 const char *wbq_last_error(const wbq_ctx *ctx);
@@ -296,6 +315,7 @@ int wbq_rbd_compute(wbq_rbd_ctx *ctx, int batch, const double *q, const double *
  * the acceleration tasks). */
 int wbq_rbd_compute_ex(wbq_rbd_ctx *ctx, int batch, const double *q, const double *qd, double *M, double *h,
                        double *J, double *pose, double *jdqd, int memory);
+/* (NULL = the model context's own stream, WBQ_NULL_STREAM = the null stream, as wbq_set_stream) */
 int wbq_rbd_set_stream(wbq_rbd_ctx *ctx, void *hip_stream);
 void wbq_rbd_destroy(wbq_rbd_ctx *ctx);
 /* MPC rollouts with the model re-evaluated every step: per step, M, h, J and

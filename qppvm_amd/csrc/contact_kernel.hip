@@ -1046,9 +1046,10 @@ hipError_t launch_t(const ContactArgs &a, hipStream_t stream, hipEvent_t mid)
     // the register slot vectors hold every active row
     if (!TR && KMR > 0 && (L.ME > KMR || a.nc * WD > KMR - 12)) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
-    // the repair kernel's LDS also holds the QR-form fallback's basis when it fits the CU's 160 KB
+    // the repair kernel's LDS also holds the QR-form fallback's basis when it fits the device's LDS per
+    // workgroup (160 KB on gfx950; queried, so a build for another target keeps the shapes that fit there)
     const size_t lds_qr = lds + sizeof(double) * QrGiLayout(L.NX, L.NX).SIZE;
-    const bool qr = lds_qr <= 160 * 1024;
+    const bool qr = lds_qr <= max_workgroup_lds();
     const size_t lds2 = qr ? lds_qr : lds;
     if (a.prepare) {
         const hipError_t e = ensure_dynamic_lds((const void *)contact_kernel<NQ, TR, KMR, WD>, lds);

@@ -39,6 +39,7 @@
 #include "qppvm_repair.h"
 
 #include <math.h>
+#include <type_traits>
 
 // Fast-kernel schedule switches (round 5; the A/B builds set them, scripts/ab_bench.py):
 //   WBQ_FAST_GJ_CH / _UNI  block_gj's trailing-read chunk and one-form update (wbq_device.h)
@@ -61,6 +62,12 @@
 #endif
 #ifndef WBQ_FAST_EQ_EARLY
 #define WBQ_FAST_EQ_EARLY 0
+#endif
+// Round 6: the n <= 32 fast path (at most two tasks, six level-0 rows) factors M by a streamed left-looking
+// block LDL^T that follows M's arrival, instead of the block Gauss-Jordan after all of M (fast_body). 0: the
+// Gauss-Jordan path (rounds 1-5), for A/B builds
+#ifndef WBQ_FAST_LDL
+#define WBQ_FAST_LDL 1
 #endif
 // dual active set, n > 32 (T rows in LDS): a dropped bound leaves the basis by Givens rotations (1) or by
 // re-projecting the later active normals (0, rounds 1-4; always for n <= 32)
@@ -94,6 +101,35 @@ struct FastLayout {
     }
 };
 
+// Streamed block LDL^T of the fast path (round 6, NP = 32, at most two tasks and six level-0 rows; see
+// fast_body): the left-looking elimination keeps every pivot block's Schur-updated column block ("panel",
+// t_j(p), rows 4p.. only) for the later blocks, instead of the Gauss-Jordan's double-buffered panel.
+// The stage-only regions (qdot, forces, poses) lie under the panels: they are dead before the first
+// panel is written (one wave per workgroup, so LDS program order is the order).
+struct LdlLayout {
+    static constexpr int NP = 32, BS = kGjBS, NBLK = NP / BS;
+    static constexpr int NB = 9;   // forward-substituted columns: 6 rows of G, J_t^T F_t - tau_imp (2), tau_imp
+    static constexpr int RHS = 12; // (row stride of the pivot rows' columns)
+    static constexpr int PANELS = BS * (NBLK * NP - BS * NBLK * (NBLK - 1) / 2); // sum_p 4 (32 - 4p) = 576
+    int JR, QD, F, PS, PL, RH, GR, LF, RES, U, SIZE;
+    // panel p starts at PL + pofs(p); row j >= 4p of it at + 4 (j - 4p)
+    __host__ __device__ static constexpr int pofs(int p) { return BS * (NP * p - BS * p * (p - 1) / 2); }
+    __host__ __device__ LdlLayout(int T, int)
+    {
+        JR = 0;                  // J rows [T*6][NP]
+        QD = JR + T * 6 * NP;    // qdot (stage)
+        F = QD + NP;             // task forces [T*6] (stage)
+        PS = F + 6 * T;          // poses [T][24] (stage)
+        PL = QD;                 // panels (over the stage regions)
+        RH = PL + PANELS;        // the pivot rows' forward-substituted columns, double-buffered [2][BS][RHS]
+        GR = RH + 2 * BS * RHS;  // Gram G G^T, lower triangle [6][kM0Max]
+        LF = GR + 6 * kM0Max;    // its factor: packed L (21), then 1 / diag (6)
+        RES = LF + 28;           // b0 - G u_imp [6] (the repair reads it)
+        U = RES + 8;             // u
+        SIZE = (U + NP + 1) & ~1;
+    }
+};
+
 // Per-instance LDS of the fast kernel: with MERGED the active-set layout reuses it afterwards
 template <int NP, bool MERGED>
 struct FastLdsLayout {
@@ -101,7 +137,12 @@ struct FastLdsLayout {
     __host__ __device__ FastLdsLayout(int T, int m0)
     {
         const int f = FastLayout<NP>(T, m0).SIZE, g = ActiveLayout<NP>(T, m0).SIZE;
-        SIZE = (MERGED && g > f) ? g : f;
+        int s = (MERGED && g > f) ? g : f;
+        if (NP == 32 && T <= 2 && m0 <= 6) { // (the streamed LDL^T variant's layout)
+            const int l = LdlLayout(T, m0).SIZE;
+            s = l > s ? l : s;
+        }
+        SIZE = s;
     }
 };
 
@@ -762,7 +803,10 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
     constexpr int IPW = kWave / NP;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int T = a.ntasks, n = a.n, m0 = a.m0;
-    const FastLayout<NP> L(T, m0);
+    // the streamed LDL^T (round 6) for the plugin's stack shape: NP = 32, two tasks, six level-0 rows
+    constexpr bool kLdl = WBQ_FAST_LDL != 0 && NP == 32 && TM == 2 && M0 == 6 && MR == 32;
+    using FL = std::conditional_t<kLdl, LdlLayout, FastLayout<NP>>;
+    const FL L(T, m0);
     int tid = threadIdx.x;
     // (a rollout step: the lane index is opaque per step, or the loop-invariant values derived from it
     // -- the identity padding of M, LDS offsets -- are hoisted out of the step loop and spilled across
@@ -839,6 +883,12 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
         Kc_i = a.Kc[fr];
         Dc_i = a.Dc[fr];
     }
+    // (LDL: the joint gains as well -- tau_imp is formed while M streams in)
+    double Kq_i = 0.0, Dq_i = 0.0;
+    if constexpr (kLdl) {
+        Kq_i = a.Kq[ic];
+        Dq_i = a.Dq[ic];
+    }
     // NP = 32, issue order pinned: the scheduler hoisted the M loads above the J loads and sank a
     // J load into the uniform branch of its LDS store, where it waited with vmcnt(0) -- for all of
     // M -- before the task forces (vmcnt retires in order). Measured (same box): n = 30 config 1
@@ -903,278 +953,533 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
         for (int r = 0; r < MR; ++r) A[r] = bload(Mrs, moff, 8 * (r < n ? r : n - 1) * n);
     }
     constexpr int NT = M0 * (M0 + 1) / 2;
-    if constexpr (WBQ_FAST_EQ_EARLY == 1) {
-        // the Gram G G^T and its factor from J alone, while M is still in flight: lane i's column of the
-        // selected J rows, per-lane outer products, instance sums by DPP (no LDS round trips); every
-        // lane factors it (rank-revealing Cholesky, dependent rows get a zero column) and lane 0 keeps
-        // the Gram (GR, lower triangle) and the factor (LF) for after the elimination
-        double g[M0];
+    // (set by either path below; u_imp and u_i by the LDL path only when an instance needs them)
+    double Y[M0];               // Y = M G^T (row i): x = tau_imp + Y c needs no second read of M
+    double tau_imp_i = 0.0, u_imp = 0.0, u_i = 0.0;
+    bool notspd = false;
+    double Lm[NT], il[M0], cv[M0]; // factor of G G^T (packed lower, row-major), c = (G G^T)^-1 res
+    double eqres = 0.0, rmx = 1.0;
+    double w_tau = 0.0;         // (LDL) this lane's entry of Dt^-1 Lt^-1 tau_imp
+    if constexpr (kLdl) {
+        // ------------------------------- 2'. streamed block LDL^T, forward substitution, Y = M G^T (round 6)
+        // M = Lt Dt Lt^T (Lt unit lower by 4 x 4 blocks, Dt block diagonal) by a LEFT-looking sweep: pivot block kb
+        // needs only M's columns 4kb..4kb+3 -- the rows this lane loaded kb-th -- and the panels of the blocks
+        // before it, so it starts as soon as its rows land while M's later rows are still in flight (vmcnt
+        // waits retire in issue order; only LDS-ordering barriers here). The Gauss-Jordan it replaces updated
+        // every column at every step, so it could not start before the last row of M (a wave
+        // waited ~11k of its ~54k cycles for M, then ran ~18k cycles of elimination).
+        //   panel p (LDS): t_j(p) = M[j][blk p] - sum_{q<p} h_j(q) . t_{blk p}(q), rows j >= 4p
+        //   D_p = t_{blk p}(p),  h_i(p) = t_i(p) D_p^-1 (rows after block p; lane i keeps it in A[4p..4p+3])
+        // The columns B = [G^T | J_t^T F_t - tau_imp | tau_imp] are forward-substituted on the way (Z = Lt^-1 B,
+        // right-looking: the pivot rows publish their final rows) and every pivot lane keeps its entries of
+        // W = Dt^-1 Z for the last three, so that
+        //   res_a = G_a M^-1 (J_t^T F_t - tau_imp) = sum_i Z_i[a] W_i[t(a)]     (one instance sum, no back sweep);
+        // u_imp = M^-1 tau_imp = Lt^-T W_tau only when an instance needs u (after the bound check).
+        constexpr int BS = LdlLayout::BS, NBLK = LdlLayout::NBLK, NB = LdlLayout::NB, RHS = LdlLayout::RHS;
+        tau_imp_i = row ? Kq_i * (qref_i - q_i) - Dq_i * qd_i : 0.0; // (:105-106)
+        lds_barrier();                                                 // the task forces
+        int rsel[M0]; // (kernel-argument words: SGPRs)
 #pragma unroll
-        for (int c = 0; c < M0; ++c) g[c] = (c < m0) ? S[L.JR + a.row_sel[c < m0 ? c : 0] * NP + i] : 0.0;
-        double gg[NT];
+        for (int c = 0; c < M0; ++c) rsel[c] = c < m0 ? a.row_selv[c] : 0;
+        double Bv[NB];
 #pragma unroll
-        for (int r = 0; r < M0; ++r)
+        for (int c = 0; c < M0; ++c) Bv[c] = c < m0 ? S[L.JR + rsel[c] * NP + i] : 0.0;
 #pragma unroll
-            for (int c = 0; c <= r; ++c) gg[r * (r + 1) / 2 + c] = g[r] * g[c];
-        isum_vec<NP, NT>(gg);
-        double Lq[NT], ilq[M0];
-        double dmx = 0.0;
+        for (int t = 0; t < TM; ++t) {
+            double c_ = 0.0;
+            if (t < T)
 #pragma unroll
-        for (int r = 0; r < M0; ++r) {
-#pragma unroll
-            for (int c = 0; c <= r; ++c) Lq[r * (r + 1) / 2 + c] = (r < m0) ? gg[r * (r + 1) / 2 + c] : 0.0;
-            dmx = fmax(dmx, Lq[r * (r + 1) / 2 + r]);
+                for (int r = 0; r < 6; ++r) c_ = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c_);
+            Bv[M0 + t] = t < T ? c_ - tau_imp_i : 0.0; // J_t^T F_t - tau_imp
         }
+        Bv[M0 + TM] = tau_imp_i;
+        // the Gram G G^T (J only) and its rank-revealing factor while M streams in; the factor waits in LDS
+        const int npairs = m0 * (m0 + 1) / 2;
+        if (i < npairs) {
+            int ra = (int)((sqrtf(8.0f * i + 1.0f) - 1.0f) * 0.5f);
+            ra += ((ra + 1) * (ra + 2) / 2 <= i) ? 1 : 0;
+            ra -= (ra * (ra + 1) / 2 > i) ? 1 : 0;
+            const int ca = i - ra * (ra + 1) / 2;
+            int r1 = rsel[0], r2 = rsel[0];
 #pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            double dd = Lq[c * (c + 1) / 2 + c];
-#pragma unroll
-            for (int k = 0; k < c; ++k) dd = fma(-Lq[c * (c + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], dd);
-            const bool indep = c < m0 && dd > 1e-12 * dmx;
-            const double ic_ = indep ? frsq(dd) : 0.0;
-            ilq[c] = ic_;
-            Lq[c * (c + 1) / 2 + c] = dd * ic_;
-#pragma unroll
-            for (int r = c + 1; r < M0; ++r) {
-                double t = Lq[r * (r + 1) / 2 + c];
-#pragma unroll
-                for (int k = 0; k < c; ++k) t = fma(-Lq[r * (r + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], t);
-                Lq[r * (r + 1) / 2 + c] = t * ic_;
+            for (int c = 1; c < M0; ++c) {
+                r1 = ra == c ? rsel[c] : r1;
+                r2 = ca == c ? rsel[c] : r2;
             }
+            S[L.GR + ra * kM0Max + ca] = dot4<MR>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
         }
-        if (i == 0) {
+        lds_barrier();
+        {
+            double dmx = 0.0;
 #pragma unroll
             for (int r = 0; r < M0; ++r) {
 #pragma unroll
-                for (int c = 0; c <= r; ++c)
-                    if (r < m0) S[L.GR + r * kM0Max + c] = gg[r * (r + 1) / 2 + c];
-                S[L.LF + NT + r] = ilq[r];
+                for (int c = 0; c <= r; ++c) Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
+                dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
             }
 #pragma unroll
-            for (int q = 0; q < NT; ++q) S[L.LF + q] = Lq[q];
-        }
-    }
-    // M (still streaming in during the forces): padding rows/columns past n -> identity
+            for (int c = 0; c < M0; ++c) {
+                double dd = Lm[c * (c + 1) / 2 + c];
 #pragma unroll
-    for (int r = 0; r < MR; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
-    // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
-    // never has to be read again (a re-read of M would double the HBM bytes of the solve)
-    double Y[M0];
-    if constexpr (WBQ_FAST_Y_CH == 0) {
+                for (int k = 0; k < c; ++k) dd = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], dd);
+                const bool indep = c < m0 && dd > 1e-12 * dmx;
+                const double ic_ = indep ? frsq(dd) : 0.0;
+                il[c] = ic_;
+                Lm[c * (c + 1) / 2 + c] = dd * ic_;
 #pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            double v = 0.0;
-            if (c < m0) {
-                const int rr = a.row_sel[c];
+                for (int r = c + 1; r < M0; ++r) {
+                    double t = Lm[r * (r + 1) / 2 + c];
 #pragma unroll
-                for (int j = 0; j < MR; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+                    for (int k = 0; k < c; ++k) t = fma(-Lm[r * (r + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], t);
+                    Lm[r * (r + 1) / 2 + c] = t * ic_;
+                }
             }
-            Y[c] = v;
-        }
-    } else {
-        // the same sums (j ascending per row), the G rows read WBQ_FAST_Y_CH columns ahead
-        constexpr int YC = WBQ_FAST_Y_CH, NYC = MR / YC;
-        static_assert(MR % YC == 0, "WBQ_FAST_Y_CH divides MR");
-        int rrs[M0];
+            if (i == 0) {
 #pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            rrs[c] = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0;
-            Y[c] = 0.0;
-        }
-        double gb[2][M0][YC];
+                for (int q = 0; q < NT; ++q) S[L.LF + q] = Lm[q];
 #pragma unroll
-        for (int ch = 0; ch <= NYC; ++ch) {
-            if (ch < NYC) {
-#pragma unroll
-                for (int c = 0; c < M0; ++c)
-#pragma unroll
-                    for (int u = 0; u < YC; ++u) gb[ch & 1][c][u] = S[L.JR + rrs[c] * NP + ch * YC + u];
+                for (int c = 0; c < M0; ++c) S[L.LF + NT + c] = il[c];
             }
-            __builtin_amdgcn_sched_barrier(0);
-            if (ch > 0) {
+        }
+        WBQ_STAMP(1); // (diagnostic: the forces and the Gram done; the sweep follows M)
+        double W3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-                for (int c = 0; c < M0; ++c)
+        for (int g = 0; g < M0; ++g) Y[g] = 0.0;
 #pragma unroll
-                    for (int u = 0; u < YC; ++u)
-                        Y[c] = fma(A[(ch - 1) * YC + u], c < m0 ? gb[(ch - 1) & 1][c][u] : 0.0, Y[c]);
+        for (int kb = 0; kb < NBLK; ++kb) {
+            const int k = kb * BS;
+            if (k < n) {
+                // (a) the earlier blocks' updates first, t_i -= h_i(p) . t_{blk kb}(p): they need the panels and
+                //     h only, so they run while this block's rows of M are still in flight. Panel p's 4 x 4 block
+                //     (rows k..k+3) is read one panel ahead of its FMAs (the compiler's own schedule waited for
+                //     every read in turn), into two accumulator sets (half the dependent chain each).
+                double ua[2][BS];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) ua[0][c] = ua[1][c] = 0.0;
+                double pv[2][BS * BS];
+                if (kb > 0) {
+#pragma unroll
+                    for (int e = 0; e < BS * BS; ++e) pv[0][e] = S[L.PL + LdlLayout::pofs(0) + BS * k + e];
+                }
+#pragma unroll
+                for (int p = 0; p < kb; ++p) {
+                    if (p + 1 < kb) {
+#pragma unroll
+                        for (int e = 0; e < BS * BS; ++e)
+                            pv[(p + 1) & 1][e] = S[L.PL + LdlLayout::pofs(p + 1) + BS * (k - BS * (p + 1)) + e];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = 0; c < BS; ++c)
+#pragma unroll
+                        for (int c2 = 0; c2 < BS; ++c2)
+                            ua[p & 1][c] = fma(A[BS * p + c2], pv[p & 1][c * BS + c2], ua[p & 1][c]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // (b) G's columns of this block (rows past m0 read row 0: their Y entries only ever meet c = 0)
+                double gk[M0][BS];
+#pragma unroll
+                for (int g = 0; g < M0; ++g)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) gk[g][c] = S[L.JR + rsel[g] * NP + k + c];
+                // (c) this block's columns of M -- the first wait for its four rows -- padding -> identity; Y += M G^T
+                double tc[BS];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) {
+                    const double raw = (row && k + c < n) ? A[k + c] : (k + c == i ? 1.0 : 0.0);
+#pragma unroll
+                    for (int g = 0; g < M0; ++g) Y[g] = fma(raw, gk[g][c], Y[g]);
+                    tc[c] = raw - (ua[0][c] + ua[1][c]);
+                }
+                const int ri = i - k;
+                const bool inK = ri >= 0 && ri < BS;
+                if (i >= k) { // panel kb, row i
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) S[L.PL + LdlLayout::pofs(kb) + BS * ri + c] = tc[c];
+                }
+                if (inK) { // the pivot rows' columns are final now (every earlier block's update is in)
+#pragma unroll
+                    for (int m = 0; m < NB; ++m) S[L.RH + (kb & 1) * BS * RHS + ri * RHS + m] = Bv[m];
+                }
+                lds_barrier();
+                // D = the pivot block of panel kb: Cholesky (redundant per lane); the pivot rows' columns are read
+                // with it (all reads issued before the factor's dependent chain)
+                const double *pd = S + L.PL + LdlLayout::pofs(kb);
+                const double *zb = S + L.RH + (kb & 1) * BS * RHS;
+                double d[BS][BS], il4[BS], zv[BS][NB];
+#pragma unroll
+                for (int r = 0; r < BS; ++r)
+#pragma unroll
+                    for (int c = 0; c <= r; ++c) d[r][c] = pd[r * BS + c];
+#pragma unroll
+                for (int r = 0; r < BS; ++r)
+#pragma unroll
+                    for (int m = 0; m < NB; ++m) zv[r][m] = zb[r * RHS + m];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < BS; ++c) {
+                    double dd = d[c][c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) dd = fma(-d[c][q_], d[c][q_], dd);
+                    notspd |= !(dd > 0.0);
+                    il4[c] = frsq(dd);
+#pragma unroll
+                    for (int r = c + 1; r < BS; ++r) {
+                        double t = d[r][c];
+#pragma unroll
+                        for (int q_ = 0; q_ < c; ++q_) t = fma(-d[r][q_], d[c][q_], t);
+                        d[r][c] = t * il4[c];
+                    }
+                }
+                // y = D^-1 t_i (rows after the block: h_i(kb)), or row ri of D^-1 (the block's own rows)
+                double y[BS];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) {
+                    double v = inK ? (ri == c ? 1.0 : 0.0) : tc[c];
+#pragma unroll
+                    for (int q_ = 0; q_ < c; ++q_) v = fma(-d[c][q_], y[q_], v);
+                    y[c] = v * il4[c];
+                }
+#pragma unroll
+                for (int c = BS - 1; c >= 0; --c) {
+                    double v = y[c];
+#pragma unroll
+                    for (int q_ = c + 1; q_ < BS; ++q_) v = fma(-d[q_][c], y[q_], v);
+                    y[c] = v * il4[c];
+                }
+                const bool later = i >= k + BS;
+#pragma unroll
+                for (int c = 0; c < BS; ++c) A[k + c] = later ? y[c] : 0.0; // h_i(kb)
+#pragma unroll
+                for (int m = 0; m < NB; ++m) {
+                    double v = Bv[m];
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) v = fma(-A[k + c], zv[c][m], v);
+                    Bv[m] = v;
+                }
+#pragma unroll
+                for (int t = 0; t < 3; ++t) { // W = D^-1 Z on the block's own rows
+                    double w = 0.0;
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) w = fma(y[c], zv[c][M0 + t], w);
+                    W3[t] = inK ? w : W3[t];
+                }
             }
-            __builtin_amdgcn_sched_barrier(0);
         }
-    }
-    __syncthreads();
-    WBQ_STAMP(1);
-
-    // ------------------------------------------ 2. block Gauss-Jordan, M SPD
-    double rhs[1 + TM];
-    rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
-    const double tau_imp_i = rhs[0];
+        WBQ_STAMP(2);
+        // ------------------------------------------ 3'. level-0 rows: G u = b0 in least distance from u_imp
+        double rv[M0];
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-        double c = 0.0;
-        if (t < T)
-#pragma unroll
-            for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
-        rhs[1 + t] = c; // J_t^T F_t
-    }
-    // (the chunked reads only where the columns leave registers for them: with 64 columns per lane they
-    // spilled, 0 -> 528 B of scratch)
-    constexpr int kGjCh = MR <= 40 ? WBQ_FAST_GJ_CH : 0;
-    bool notspd = block_gj<NP, 1 + TM, 8, MR, kGjCh, WBQ_FAST_GJ_UNI != 0>(A, rhs, n, i, S + L.PN, S + L.RH);
-    const double u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
-    double gq[NT], resq[M0]; // (EQ_EARLY == 2) the Gram and res in registers
-    if constexpr (!WBQ_FAST_EQ_EARLY) {
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-            if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
-        __syncthreads();
-    }
-    WBQ_STAMP(2);
-
-    // ------------------------------ 3. level-0 rows: G u = b0 in least distance from u_imp
-    // res_a = b0_a - G_a u_imp = G_a (w_t(a) - u_imp), and the Gram G G^T: one dot per lane
-    if constexpr (WBQ_FAST_EQ_EARLY == 2) {
-        // res and the Gram by per-lane products (lane i's column of the selected J rows), one DPP
-        // reduction of the NT + M0 sums; no LDS round trip
-        double g[M0], v[NT + M0];
-#pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
-            g[c] = c < m0 ? S[L.JR + rr * NP + i] : 0.0;
-            double w = rhs[1];
-#pragma unroll
-            for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
-            v[NT + c] = g[c] * (w - u_imp);
-        }
-#pragma unroll
-        for (int r = 0; r < M0; ++r)
-#pragma unroll
-            for (int c = 0; c <= r; ++c) v[r * (r + 1) / 2 + c] = g[r] * g[c];
-        isum_vec<NP, NT + M0>(v);
-#pragma unroll
-        for (int q = 0; q < NT; ++q) gq[q] = v[q];
-#pragma unroll
-        for (int c = 0; c < M0; ++c) resq[c] = v[NT + c];
+        for (int c = 0; c < M0; ++c) rv[c] = c < m0 ? Bv[c] * ((rsel[c] >= 6) ? W3[1] : W3[0]) : 0.0;
+        isum_vec<NP, M0>(rv);
         if (i < m0) { // (the repair path's b0 reads res from LDS)
-            double rv = 0.0;
+            double v = 0.0;
 #pragma unroll
-            for (int c = 0; c < M0; ++c) rv = i == c ? resq[c] : rv;
-            S[L.RES + i] = rv;
+            for (int c = 0; c < M0; ++c) v = i == c ? rv[c] : v;
+            S[L.RES + i] = v;
         }
-    } else if constexpr (WBQ_FAST_EQ_EARLY == 1) {
-        // (the Gram and its factor are in LDS since the stage) res by per-lane products and DPP sums
-        double rp[M0];
+        w_tau = W3[2];
+        double rs[M0];
 #pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
-            double w = rhs[1];
-#pragma unroll
-            for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
-            rp[c] = c < m0 ? S[L.JR + rr * NP + i] * (w - u_imp) : 0.0;
-        }
-        isum_vec<NP, M0>(rp);
-        if (i == 0) {
-#pragma unroll
-            for (int c = 0; c < M0; ++c)
-                if (c < m0) S[L.RES + c] = rp[c];
-        }
-        __syncthreads();
-    } else {
-        const int npairs = m0 * (m0 + 1) / 2;
-        for (int pp = i; pp < npairs + m0; pp += NP) {
-            if (pp < m0) {
-                const int rr = a.row_sel[pp], t = rr / 6;
-                S[L.RES + pp] = dot4<MR>(S + L.JR + rr * NP, S + L.WV + t * NP);
-            } else {
-                const int p2 = pp - m0;
-                int ra = (int)((sqrtf(8.0f * p2 + 1.0f) - 1.0f) * 0.5f);
-                ra += ((ra + 1) * (ra + 2) / 2 <= p2) ? 1 : 0;
-                ra -= (ra * (ra + 1) / 2 > p2) ? 1 : 0;
-                const int ca = p2 - ra * (ra + 1) / 2;
-                const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
-                S[L.GR + ra * kM0Max + ca] = dot4<MR>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
-            }
-        }
-        __syncthreads();
-    }
-    // Every lane factors the small Gram redundantly in registers: rank-revealing Cholesky
-    // G G^T = L L^T (dependent rows get a zero column), c = L^-T L^-1 res, u = u_imp + G^T c.
-    double Lm[M0 * (M0 + 1) / 2]; // packed lower triangle, row-major
-    double il[M0], rs[M0];
-    if constexpr (WBQ_FAST_EQ_EARLY == 1) {
-#pragma unroll
-        for (int r = 0; r < M0; ++r) {
-            rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
-            il[r] = S[L.LF + NT + r];
-        }
+        for (int r = 0; r < M0; ++r) rs[r] = (r < m0) ? rv[r] : 0.0;
 #pragma unroll
         for (int q = 0; q < NT; ++q) Lm[q] = S[L.LF + q];
-    } else {
-        double dmx = 0.0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) il[c] = S[L.LF + NT + c];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) { // forward: rho = L^-1 res
+            double v = rs[c];
+#pragma unroll
+            for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], cv[k], v);
+            cv[c] = v * il[c];
+        }
+#pragma unroll
+        for (int c = M0 - 1; c >= 0; --c) { // backward: c = L^-T rho
+            double v = cv[c];
+#pragma unroll
+            for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
+            cv[c] = v * il[c];
+        }
+        // consistency of the level-0 rows (rows dropped as dependent must still be met, else y* != b0)
 #pragma unroll
         for (int r = 0; r < M0; ++r) {
-            if constexpr (WBQ_FAST_EQ_EARLY == 2) rs[r] = (r < m0) ? resq[r] : 0.0;
-            else rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
+            double v = -rs[r];
 #pragma unroll
-            for (int c = 0; c <= r; ++c) {
-                if constexpr (WBQ_FAST_EQ_EARLY == 2) Lm[r * (r + 1) / 2 + c] = (r < m0) ? gq[r * (r + 1) / 2 + c] : 0.0;
-                else Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
-            }
-            dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
-        }
-#pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            double dd = Lm[c * (c + 1) / 2 + c];
-#pragma unroll
-            for (int k = 0; k < c; ++k) dd = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], dd);
-            const bool indep = c < m0 && dd > 1e-12 * dmx;
-            const double ic_ = indep ? frsq(dd) : 0.0;
-            il[c] = ic_;
-            Lm[c * (c + 1) / 2 + c] = dd * ic_;
-#pragma unroll
-            for (int r = c + 1; r < M0; ++r) {
-                double t = Lm[r * (r + 1) / 2 + c];
-#pragma unroll
-                for (int k = 0; k < c; ++k) t = fma(-Lm[r * (r + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], t);
-                Lm[r * (r + 1) / 2 + c] = t * ic_;
-            }
-        }
-    }
-    double cv[M0];
-#pragma unroll
-    for (int c = 0; c < M0; ++c) { // forward: rho = L^-1 res
-        double v = rs[c];
-#pragma unroll
-        for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], cv[k], v);
-        cv[c] = v * il[c];
-    }
-#pragma unroll
-    for (int c = M0 - 1; c >= 0; --c) { // backward: c = L^-T rho
-        double v = cv[c];
-#pragma unroll
-        for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
-        cv[c] = v * il[c];
-    }
-    // consistency of the level-0 rows (rows dropped as dependent must still be met,
-    // otherwise y* != b0: level 0 infeasible)
-    double eqres = 0.0, rmx = 1.0;
-#pragma unroll
-    for (int r = 0; r < M0; ++r) {
-        double v = -rs[r];
-#pragma unroll
-        for (int c = 0; c < M0; ++c) {
-            if constexpr (WBQ_FAST_EQ_EARLY == 2) {
-                if (r < m0 && c < m0) v = fma(gq[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r], cv[c], v);
-            } else {
+            for (int c = 0; c < M0; ++c)
                 if (r < m0 && c < m0) v = fma(S[L.GR + (r >= c ? r * kM0Max + c : c * kM0Max + r)], cv[c], v);
+            eqres = fmax(eqres, fabs(v));
+            rmx = fmax(rmx, fabs(rs[r]));
+        }
+    } else {
+        if constexpr (WBQ_FAST_EQ_EARLY == 1) {
+            // the Gram G G^T and its factor from J alone, while M is still in flight: lane i's column of the
+            // selected J rows, per-lane outer products, instance sums by DPP (no LDS round trips); every
+            // lane factors it (rank-revealing Cholesky, dependent rows get a zero column) and lane 0 keeps
+            // the Gram (GR, lower triangle) and the factor (LF) for after the elimination
+            double g[M0];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) g[c] = (c < m0) ? S[L.JR + a.row_sel[c < m0 ? c : 0] * NP + i] : 0.0;
+            double gg[NT];
+    #pragma unroll
+            for (int r = 0; r < M0; ++r)
+    #pragma unroll
+                for (int c = 0; c <= r; ++c) gg[r * (r + 1) / 2 + c] = g[r] * g[c];
+            isum_vec<NP, NT>(gg);
+            double Lq[NT], ilq[M0];
+            double dmx = 0.0;
+    #pragma unroll
+            for (int r = 0; r < M0; ++r) {
+    #pragma unroll
+                for (int c = 0; c <= r; ++c) Lq[r * (r + 1) / 2 + c] = (r < m0) ? gg[r * (r + 1) / 2 + c] : 0.0;
+                dmx = fmax(dmx, Lq[r * (r + 1) / 2 + r]);
+            }
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                double dd = Lq[c * (c + 1) / 2 + c];
+    #pragma unroll
+                for (int k = 0; k < c; ++k) dd = fma(-Lq[c * (c + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], dd);
+                const bool indep = c < m0 && dd > 1e-12 * dmx;
+                const double ic_ = indep ? frsq(dd) : 0.0;
+                ilq[c] = ic_;
+                Lq[c * (c + 1) / 2 + c] = dd * ic_;
+    #pragma unroll
+                for (int r = c + 1; r < M0; ++r) {
+                    double t = Lq[r * (r + 1) / 2 + c];
+    #pragma unroll
+                    for (int k = 0; k < c; ++k) t = fma(-Lq[r * (r + 1) / 2 + k], Lq[c * (c + 1) / 2 + k], t);
+                    Lq[r * (r + 1) / 2 + c] = t * ic_;
+                }
+            }
+            if (i == 0) {
+    #pragma unroll
+                for (int r = 0; r < M0; ++r) {
+    #pragma unroll
+                    for (int c = 0; c <= r; ++c)
+                        if (r < m0) S[L.GR + r * kM0Max + c] = gg[r * (r + 1) / 2 + c];
+                    S[L.LF + NT + r] = ilq[r];
+                }
+    #pragma unroll
+                for (int q = 0; q < NT; ++q) S[L.LF + q] = Lq[q];
             }
         }
-        eqres = fmax(eqres, fabs(v));
-        rmx = fmax(rmx, fabs(rs[r]));
+        // M (still streaming in during the forces): padding rows/columns past n -> identity
+    #pragma unroll
+        for (int r = 0; r < MR; ++r) A[r] = (row && r < n) ? A[r] : (r == i ? 1.0 : 0.0);
+        // Y = M G^T (row i per lane): then x = M u = tau_imp + Y c after the elimination, and M
+        // never has to be read again (a re-read of M would double the HBM bytes of the solve)
+        if constexpr (WBQ_FAST_Y_CH == 0) {
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                double v = 0.0;
+                if (c < m0) {
+                    const int rr = a.row_sel[c];
+    #pragma unroll
+                    for (int j = 0; j < MR; ++j) v = fma(A[j], S[L.JR + rr * NP + j], v);
+                }
+                Y[c] = v;
+            }
+        } else {
+            // the same sums (j ascending per row), the G rows read WBQ_FAST_Y_CH columns ahead
+            constexpr int YC = WBQ_FAST_Y_CH, NYC = MR / YC;
+            static_assert(MR % YC == 0, "WBQ_FAST_Y_CH divides MR");
+            int rrs[M0];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                rrs[c] = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0;
+                Y[c] = 0.0;
+            }
+            double gb[2][M0][YC];
+    #pragma unroll
+            for (int ch = 0; ch <= NYC; ++ch) {
+                if (ch < NYC) {
+    #pragma unroll
+                    for (int c = 0; c < M0; ++c)
+    #pragma unroll
+                        for (int u = 0; u < YC; ++u) gb[ch & 1][c][u] = S[L.JR + rrs[c] * NP + ch * YC + u];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (ch > 0) {
+    #pragma unroll
+                    for (int c = 0; c < M0; ++c)
+    #pragma unroll
+                        for (int u = 0; u < YC; ++u)
+                            Y[c] = fma(A[(ch - 1) * YC + u], c < m0 ? gb[(ch - 1) & 1][c][u] : 0.0, Y[c]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();
+        WBQ_STAMP(1);
+
+        // ------------------------------------------ 2. block Gauss-Jordan, M SPD
+        double rhs[1 + TM];
+        rhs[0] = row ? a.Kq[ic] * (qref_i - q_i) - a.Dq[ic] * qd_i : 0.0; // tau_imp (:105-106)
+        tau_imp_i = rhs[0];
+    #pragma unroll
+        for (int t = 0; t < TM; ++t) {
+            double c = 0.0;
+            if (t < T)
+    #pragma unroll
+                for (int r = 0; r < 6; ++r) c = fma(S[L.JR + (t * 6 + r) * NP + i], S[L.F + t * 6 + r], c);
+            rhs[1 + t] = c; // J_t^T F_t
+        }
+        // (the chunked reads only where the columns leave registers for them: with 64 columns per lane they
+        // spilled, 0 -> 528 B of scratch)
+        constexpr int kGjCh = MR <= 40 ? WBQ_FAST_GJ_CH : 0;
+        notspd = block_gj<NP, 1 + TM, 8, MR, kGjCh, WBQ_FAST_GJ_UNI != 0>(A, rhs, n, i, S + L.PN, S + L.RH);
+        u_imp = rhs[0]; // u_imp = M^-1 tau_imp, w_t = M^-1 J_t^T F_t = rhs[1+t]
+        double gq[NT], resq[M0]; // (EQ_EARLY == 2) the Gram and res in registers
+        if constexpr (!WBQ_FAST_EQ_EARLY) {
+    #pragma unroll
+            for (int t = 0; t < TM; ++t)
+                if (t < T) S[L.WV + t * NP + i] = rhs[1 + t] - u_imp;
+            __syncthreads();
+        }
+        WBQ_STAMP(2);
+
+        // ------------------------------ 3. level-0 rows: G u = b0 in least distance from u_imp
+        // res_a = b0_a - G_a u_imp = G_a (w_t(a) - u_imp), and the Gram G G^T: one dot per lane
+        if constexpr (WBQ_FAST_EQ_EARLY == 2) {
+            // res and the Gram by per-lane products (lane i's column of the selected J rows), one DPP
+            // reduction of the NT + M0 sums; no LDS round trip
+            double g[M0], v[NT + M0];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
+                g[c] = c < m0 ? S[L.JR + rr * NP + i] : 0.0;
+                double w = rhs[1];
+    #pragma unroll
+                for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
+                v[NT + c] = g[c] * (w - u_imp);
+            }
+    #pragma unroll
+            for (int r = 0; r < M0; ++r)
+    #pragma unroll
+                for (int c = 0; c <= r; ++c) v[r * (r + 1) / 2 + c] = g[r] * g[c];
+            isum_vec<NP, NT + M0>(v);
+    #pragma unroll
+            for (int q = 0; q < NT; ++q) gq[q] = v[q];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) resq[c] = v[NT + c];
+            if (i < m0) { // (the repair path's b0 reads res from LDS)
+                double rv = 0.0;
+    #pragma unroll
+                for (int c = 0; c < M0; ++c) rv = i == c ? resq[c] : rv;
+                S[L.RES + i] = rv;
+            }
+        } else if constexpr (WBQ_FAST_EQ_EARLY == 1) {
+            // (the Gram and its factor are in LDS since the stage) res by per-lane products and DPP sums
+            double rp[M0];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                const int rr = c < m0 ? a.row_sel[c < m0 ? c : 0] : 0, tt = rr / 6;
+                double w = rhs[1];
+    #pragma unroll
+                for (int t = 1; t < TM; ++t) w = tt == t ? rhs[1 + t] : w;
+                rp[c] = c < m0 ? S[L.JR + rr * NP + i] * (w - u_imp) : 0.0;
+            }
+            isum_vec<NP, M0>(rp);
+            if (i == 0) {
+    #pragma unroll
+                for (int c = 0; c < M0; ++c)
+                    if (c < m0) S[L.RES + c] = rp[c];
+            }
+            __syncthreads();
+        } else {
+            const int npairs = m0 * (m0 + 1) / 2;
+            for (int pp = i; pp < npairs + m0; pp += NP) {
+                if (pp < m0) {
+                    const int rr = a.row_sel[pp], t = rr / 6;
+                    S[L.RES + pp] = dot4<MR>(S + L.JR + rr * NP, S + L.WV + t * NP);
+                } else {
+                    const int p2 = pp - m0;
+                    int ra = (int)((sqrtf(8.0f * p2 + 1.0f) - 1.0f) * 0.5f);
+                    ra += ((ra + 1) * (ra + 2) / 2 <= p2) ? 1 : 0;
+                    ra -= (ra * (ra + 1) / 2 > p2) ? 1 : 0;
+                    const int ca = p2 - ra * (ra + 1) / 2;
+                    const int r1 = a.row_sel[ra], r2 = a.row_sel[ca];
+                    S[L.GR + ra * kM0Max + ca] = dot4<MR>(S + L.JR + r1 * NP, S + L.JR + r2 * NP);
+                }
+            }
+            __syncthreads();
+        }
+        // Every lane factors the small Gram redundantly in registers: rank-revealing Cholesky
+        // G G^T = L L^T (dependent rows get a zero column), c = L^-T L^-1 res, u = u_imp + G^T c.
+        double rs[M0];
+        if constexpr (WBQ_FAST_EQ_EARLY == 1) {
+    #pragma unroll
+            for (int r = 0; r < M0; ++r) {
+                rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
+                il[r] = S[L.LF + NT + r];
+            }
+    #pragma unroll
+            for (int q = 0; q < NT; ++q) Lm[q] = S[L.LF + q];
+        } else {
+            double dmx = 0.0;
+    #pragma unroll
+            for (int r = 0; r < M0; ++r) {
+                if constexpr (WBQ_FAST_EQ_EARLY == 2) rs[r] = (r < m0) ? resq[r] : 0.0;
+                else rs[r] = (r < m0) ? S[L.RES + r] : 0.0;
+    #pragma unroll
+                for (int c = 0; c <= r; ++c) {
+                    if constexpr (WBQ_FAST_EQ_EARLY == 2) Lm[r * (r + 1) / 2 + c] = (r < m0) ? gq[r * (r + 1) / 2 + c] : 0.0;
+                    else Lm[r * (r + 1) / 2 + c] = (r < m0) ? S[L.GR + r * kM0Max + c] : 0.0;
+                }
+                dmx = fmax(dmx, Lm[r * (r + 1) / 2 + r]);
+            }
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                double dd = Lm[c * (c + 1) / 2 + c];
+    #pragma unroll
+                for (int k = 0; k < c; ++k) dd = fma(-Lm[c * (c + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], dd);
+                const bool indep = c < m0 && dd > 1e-12 * dmx;
+                const double ic_ = indep ? frsq(dd) : 0.0;
+                il[c] = ic_;
+                Lm[c * (c + 1) / 2 + c] = dd * ic_;
+    #pragma unroll
+                for (int r = c + 1; r < M0; ++r) {
+                    double t = Lm[r * (r + 1) / 2 + c];
+    #pragma unroll
+                    for (int k = 0; k < c; ++k) t = fma(-Lm[r * (r + 1) / 2 + k], Lm[c * (c + 1) / 2 + k], t);
+                    Lm[r * (r + 1) / 2 + c] = t * ic_;
+                }
+            }
+        }
+    #pragma unroll
+        for (int c = 0; c < M0; ++c) { // forward: rho = L^-1 res
+            double v = rs[c];
+    #pragma unroll
+            for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], cv[k], v);
+            cv[c] = v * il[c];
+        }
+    #pragma unroll
+        for (int c = M0 - 1; c >= 0; --c) { // backward: c = L^-T rho
+            double v = cv[c];
+    #pragma unroll
+            for (int k = c + 1; k < M0; ++k) v = fma(-Lm[k * (k + 1) / 2 + c], cv[k], v);
+            cv[c] = v * il[c];
+        }
+        // consistency of the level-0 rows (rows dropped as dependent must still be met,
+        // otherwise y* != b0: level 0 infeasible)
+    #pragma unroll
+        for (int r = 0; r < M0; ++r) {
+            double v = -rs[r];
+    #pragma unroll
+            for (int c = 0; c < M0; ++c) {
+                if constexpr (WBQ_FAST_EQ_EARLY == 2) {
+                    if (r < m0 && c < m0) v = fma(gq[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r], cv[c], v);
+                } else {
+                    if (r < m0 && c < m0) v = fma(S[L.GR + (r >= c ? r * kM0Max + c : c * kM0Max + r)], cv[c], v);
+                }
+            }
+            eqres = fmax(eqres, fabs(v));
+            rmx = fmax(rmx, fabs(rs[r]));
+        }
+        u_i = u_imp;
+    #pragma unroll
+        for (int c = 0; c < M0; ++c)
+            if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
     }
-    double u_i = u_imp;
-#pragma unroll
-    for (int c = 0; c < M0; ++c)
-        if (c < m0) u_i = fma(S[L.JR + a.row_sel[c] * NP + i], cv[c], u_i);
     WBQ_STAMP(3);
 
     // ------------------------------------------------------------ 4. bound check
@@ -1200,6 +1505,35 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
     flag = imax<NP>(flag);
     if (flag >= 2.0 && status == 0) status = 3;
     const bool active = (flag > 0.0 || l0bad) && status == 0 && valid;
+    if constexpr (kLdl) {
+        // u_imp = M^-1 tau_imp = Lt^-T (Dt^-1 Lt^-1 tau_imp) and u = u_imp + G^T c, only when some instance of
+        // the wave needs u: a rollout integrates qdd = u, an active bound or a level-0 repair starts from it
+        // (the common path needs x alone). Block kb from the last: u_blk = w_blk - sum_{later rows i} h_i(kb) u_i.
+        if (a.integrate || __any(active)) {
+            constexpr int BS = LdlLayout::BS, NBLK = LdlLayout::NBLK;
+            double uu = 0.0;
+#pragma unroll
+            for (int kb = NBLK - 1; kb >= 0; --kb) {
+                const int k = kb * BS;
+                if (k < n) {
+                    double s4[BS];
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) s4[c] = A[k + c] * uu;
+                    isum_vec<NP, BS>(s4);
+                    const int ri = i - k;
+                    double sv = 0.0;
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) sv = ri == c ? s4[c] : sv;
+                    if (ri >= 0 && ri < BS) uu = w_tau - sv;
+                }
+            }
+            u_imp = uu;
+            u_i = u_imp;
+#pragma unroll
+            for (int c = 0; c < M0; ++c)
+                if (c < m0) u_i = fma(S[L.JR + a.row_selv[c] * NP + i], cv[c], u_i);
+        }
+    }
     if (__any(active)) { // b0 = res + G u_imp for the level-0 repair
         S[L.U + i] = u_imp;
         __syncthreads();

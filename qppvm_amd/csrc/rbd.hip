@@ -483,7 +483,7 @@ int wbq_rbd_create(const wbq_rbd_desc *d, int device, wbq_rbd_ctx **out)
 int wbq_rbd_set_stream(wbq_rbd_ctx *c, void *hip_stream)
 {
     if (!c) return WBQ_E_INVALID;
-    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+    c->stream = hip_stream == WBQ_NULL_STREAM ? (hipStream_t)0 : hip_stream ? (hipStream_t)hip_stream : c->own_stream;
     return WBQ_SUCCESS;
 }
 

@@ -39,6 +39,7 @@ struct wbq_ctx {
     // batch-shared parameters (device)
     double *Kc = nullptr, *Dc = nullptr, *Kq = nullptr, *Dq = nullptr, *tmax = nullptr, *tmin = nullptr;
     int *row_sel = nullptr;
+    int row_sel_host[wbq::kM0Max] = {}; // the same, passed by value in the kernel argument
     // owned inputs: one device block + one pinned host staging block, fields packed back to
     // back for the current batch, so a host-side set_inputs is a single H2D copy
     double *dev_in = nullptr, *host_in = nullptr;
@@ -51,6 +52,7 @@ struct wbq_ctx {
     int nx = 0;
     int batch = 0;
     bool have_inputs = false;
+    bool inputs_device = false; // the current inputs are the caller's WBQ_MEM_DEVICE buffers
     // outputs: one device block [tau | status | iters] packed for the current batch (single
     // D2H copy into the pinned host block), and optional caller-owned device buffers
     double *dev_out = nullptr, *host_out = nullptr;
@@ -116,6 +118,25 @@ hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes)
     e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) cur = bytes;
     return e;
+}
+
+size_t max_workgroup_lds()
+{
+    static std::mutex mu;
+    static std::map<int, size_t> seen; // device -> bytes
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 64 * 1024;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = seen.find(dev);
+    if (it != seen.end()) return it->second;
+    // (the opt-in limit is what hipFuncSetAttribute can raise a kernel to; the larger of the two)
+    int v = 0, o = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) v = 0;
+    if (hipDeviceGetAttribute(&o, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) o = 0;
+    const int m = v > o ? v : o;
+    const size_t bytes = m > 0 ? (size_t)m : 64 * 1024;
+    seen[dev] = bytes;
+    return bytes;
 }
 
 }  // namespace wbq
@@ -376,6 +397,7 @@ int wbq_create(const wbq_desc *desc, int device, wbq_ctx **out)
          hipMemcpy(c->tmin, d.tau_min, n * 8, hipMemcpyHostToDevice) == hipSuccess &&
          hipMemcpy(c->row_sel, sel, sizeof(int) * m0, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) return cleanup(WBQ_E_DEVICE);
+    for (int r = 0; r < m0; ++r) c->row_sel_host[r] = sel[r];
     {
         // scratch lanes per instance (the W1 = M repair runs one instance per wave)
         const size_t np = cspace ? 64 : (size_t)wbq::lanes_per_instance(d.n);
@@ -536,7 +558,7 @@ int wbq_set_stream(wbq_ctx *c, void *hip_stream)
 {
     if (!c) return WBQ_E_INVALID;
     if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
-    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+    c->stream = hip_stream == WBQ_NULL_STREAM ? (hipStream_t)0 : hip_stream ? (hipStream_t)hip_stream : c->own_stream;
     return WBQ_SUCCESS;
 }
 
@@ -553,6 +575,7 @@ int wbq_set_inputs(wbq_ctx *c, const wbq_inputs *in)
     if (in->memory != WBQ_MEM_DEVICE && in->memory != WBQ_MEM_HOST)
         return fail(c, WBQ_E_INVALID, "unknown memory kind");
     WBQ_HIP(hipSetDevice(c->device));
+    c->inputs_device = in->memory == WBQ_MEM_DEVICE;
     if (in->memory == WBQ_MEM_DEVICE) {
         for (int f = 0; f < 8; ++f) c->in[f] = src[f];
     } else {
@@ -611,6 +634,7 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
     a.limits_crossed = c->limits_crossed;
     for (int t = 0; t < wbq::kTMax; ++t) a.row_mask[t] = t < c->d.ntasks ? c->d.row_mask[t] : 0;
     a.row_sel = c->row_sel;
+    for (int r = 0; r < wbq::kM0Max; ++r) a.row_selv[r] = c->row_sel_host[r];
     a.Kc = c->Kc;
     a.Dc = c->Dc;
     a.Kq = c->Kq;
@@ -669,8 +693,11 @@ static int solve_impl(wbq_ctx *c, int integrate, double dt, bool prepare = false
         // merged path enqueues the fast kernel alone (an empty follow-up launch costs ~1.5-3 us of a
         // ~35 us config-1 step); a solve that did list one is completed when its outputs are read
         // (complete_pending). Not with caller-owned device outputs (a stream consumer would read them
-        // before that), rollouts, rbd re-evaluation, or the constraint-space and inline variants.
+        // before that), caller-owned device inputs (the deferred repair would read them when the outputs
+        // are read, after the caller may have refilled them on the stream), rollouts, rbd re-evaluation,
+        // or the constraint-space and inline variants.
         a.skip_followup = (c->opt_followup == 1 && !prepare && !integrate && steps == 0 && !rbd && a.B > 0 &&
+                           !c->inputs_device &&
                            c->d.n <= 32 && c->d.joint_weight == WBQ_WEIGHT_IDENTITY && !c->d.no_joint_task &&
                            !a.inline_repair && !c->out_tau && !c->out_status && !c->out_iters && seen1 == 0 &&
                            c->fest[1] == 0) ? 1 : 0;
@@ -721,6 +748,16 @@ int wbq_set_option(wbq_ctx *c, int option, int value)
         if (value < 0 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_FOLLOWUP: 0 or 1");
         if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
         c->opt_followup = value;
+        return WBQ_SUCCESS;
+    case WBQ_OPT_HANDBACK:
+        if (value < 0 || value > 1) return fail(c, WBQ_E_INVALID, "WBQ_OPT_HANDBACK: 0 or 1");
+        if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
+        c->opt_handback = value;
+        return WBQ_SUCCESS;
+    case WBQ_OPT_GI_HANDOFF:
+        if (value < 0) return fail(c, WBQ_E_INVALID, "WBQ_OPT_GI_HANDOFF: >= 0");
+        if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
+        c->opt_handoff = value;
         return WBQ_SUCCESS;
     default:
         return fail(c, WBQ_E_INVALID, "wbq_set_option: unknown option");
@@ -884,6 +921,8 @@ int wbq_reset_warmstart(wbq_ctx *c, const uint8_t *mask)
     // Drops the per-instance warm start (repair hint, BVLS bound state, the dual loop's last
     // active set), stream-ordered with the solves; a cold instance takes the default path next time.
     if (!c) return WBQ_E_INVALID;
+    // a solve left pending (on-demand follow-up) first: its deferred repair writes the warm-start state
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     if (!c->ws_hint && !c->ws_rows) return WBQ_SUCCESS; // no warm-start state in this form
     WBQ_HIP(hipSetDevice(c->device));
     const int B = mask ? c->batch : c->d.max_batch; // a mask has one entry per instance of the batch
@@ -924,6 +963,8 @@ int wbq_get_warmstart_hints(wbq_ctx *c, uint8_t *hints)
 int wbq_set_timing(wbq_ctx *c, int enable)
 {
     if (!c) return WBQ_E_INVALID;
+    // (a pending solve's deferred repair belongs to the solves before this window, not to the timed ones)
+    if (complete_pending(c) != WBQ_SUCCESS) return WBQ_E_DEVICE;
     WBQ_HIP(hipSetDevice(c->device));
     if (enable && c->ev.empty()) {
         c->ev.resize(3 * 4096);

@@ -56,6 +56,9 @@ struct QppvmArgs {
     int limits_crossed; // some tau_min > tau_max (batch-shared limits): every instance infeasible
     int row_mask[kTMax];
     const int *row_sel;      // [m0] task-row index t*6+r of level-0 row a (device)
+    // the same by value: kernel-argument words are scalar loads (lgkmcnt), where a read through row_sel after
+    // the stage's M loads is a vector load, and waiting for it waits for all of M (vmcnt retires in order)
+    int row_selv[kM0Max];
     const double *Kc, *Dc;   // [ntasks*6] (device)
     const double *Kq, *Dq;   // [n]
     const double *tau_max, *tau_min; // [n]
@@ -146,6 +149,9 @@ constexpr int kStamps = 64;
 // device and kernel; thread-safe: contexts on several devices or threads share it). Called only
 // by the launchers' prepare pass (wbq_create*), never on the solve path.
 hipError_t ensure_dynamic_lds(const void *kernel, size_t bytes);
+// LDS bytes one workgroup may use on the current device (hipDeviceAttributeMaxSharedMemoryPerBlock or the
+// opt-in limit, the larger; cached per device; 64 KB if the query fails)
+size_t max_workgroup_lds();
 
 // Launch the fused QPPVM solve (assemble -> 2-level hierarchical QP -> tau) for a batch.
 // mid (optional): recorded on the stream right after the first (dominant) kernel.

@@ -219,7 +219,7 @@ class RBDModel:
             raise wbq.WbqError(f"wbq_rbd_compute failed ({rc})")
 
     def set_stream(self, stream_handle):
-        self.lib.wbq_rbd_set_stream(self.ctx, stream_handle or None)
+        self.lib.wbq_rbd_set_stream(self.ctx, wbq.stream_arg(stream_handle))
 
     def close(self):
         if getattr(self, "ctx", None):

@@ -18,6 +18,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libwbq.so")
 
 SUCCESS, E_INVALID, E_DEVICE, E_UNSUPPORTED, E_CAPACITY = 0, -1, -2, -3, -4
+NULL_STREAM = 1  # include/wbq.h WBQ_NULL_STREAM: the device's null stream (torch's default, handle 0)
+
+
+def stream_arg(handle):
+    """wbq_set_stream argument for a stream handle: None -> the context's own stream, 0 (the null
+    stream, e.g. torch.cuda.current_stream().cuda_stream of the default stream) -> WBQ_NULL_STREAM."""
+    if handle is None:
+        return None
+    return NULL_STREAM if int(handle) == 0 else int(handle)
 MEM_HOST, MEM_DEVICE = 0, 1
 FORM_QPPVM, FORM_CONTACT = 0, 1
 
@@ -217,7 +226,9 @@ class QPPVMSolver:
         self.batch = int(batch)
 
     def set_stream(self, stream_handle: int | None):
-        self._check(self.lib.wbq_set_stream(self.ctx, stream_handle or None), "wbq_set_stream")
+        """Launch on this HIP stream handle (None: the context's own stream; 0: the null stream, which is
+        torch's default stream)."""
+        self._check(self.lib.wbq_set_stream(self.ctx, stream_arg(stream_handle)), "wbq_set_stream")
 
     # -- solve
     def solve(self):
@@ -249,6 +260,8 @@ class QPPVMSolver:
     OPT_INLINE_REPAIR = 1  # include/wbq.h WBQ_OPT_*
     OPT_FUSED_ROLLOUT = 2
     OPT_FOLLOWUP = 3  # on-demand follow-up kernel (completed when outputs are read)
+    OPT_HANDBACK = 4  # n > 32: a repaired instance's dual loop in the hand-back pass
+    OPT_GI_HANDOFF = 5  # n > 32: active-set steps before the level-0 repair takes over (0 = never)
 
     def set_option(self, option: int, value: int):
         """Per-context execution option (wbq_set_option): a path choice, never a result change."""

@@ -79,11 +79,65 @@ def test_followup_deferred_completion(wbq_mod, oracle_lib):
         np.testing.assert_array_equal(st, st_r)
         ok = st_r == 0
         assert rel_err(tau[ok], tau_r[ok]) <= TOL
-        # solve twice without reading: the second supersedes the first, outputs read once at the end
-        s.solve()
-        s.solve()
-        tau2, st2, _ = s.outputs()
-        np.testing.assert_array_equal(st2, st_r)
-        assert rel_err(tau2[ok], tau_r[ok]) <= TOL
     finally:
         s.close()
+
+
+def test_followup_superseded_pending_solve(wbq_mod, oracle_lib):
+    """A fresh context starts in the on-demand mode: two solves of the repair-heavy batch without a read in
+    between leave the first pending and let the second supersede it (its listing flag, the stale counters
+    the second solve's fast kernel clears); the outputs read once at the end equal OPT_FOLLOWUP = 0 bit for
+    bit, and a third solve after the read (now with the follow-up enqueued) agrees too."""
+    tight, _, _, heavy = cases(oracle_lib)
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(tight, heavy)
+    ref = wbq_mod.QPPVMSolver(tight, max_batch=64)
+    try:
+        ref.set_option(ref.OPT_FOLLOWUP, 0)
+        t0, s0, i0 = ref.solve_batch(heavy)
+    finally:
+        ref.close()
+    s = wbq_mod.QPPVMSolver(tight, max_batch=64)
+    try:
+        s.set_option(s.OPT_FOLLOWUP, 1)
+        s.set_inputs(heavy)
+        s.solve()
+        s.solve()
+        t1, s1, i1 = s.outputs()
+        s.solve()
+        t2, s2, i2 = s.outputs()
+    finally:
+        s.close()
+    np.testing.assert_array_equal(s1, s0)
+    np.testing.assert_array_equal(t1, t0)
+    np.testing.assert_array_equal(s1, st_r)
+    ok = st_r == 0
+    assert rel_err(t1[ok], tau_r[ok]) <= TOL
+    # (the third solve starts warm from the second: the path may change, the solution may not)
+    np.testing.assert_array_equal(s2, st_r)
+    assert rel_err(t2[ok], tau_r[ok]) <= TOL
+
+
+def test_followup_device_inputs_refilled_after_solve(wbq_mod, oracle_lib):
+    """WBQ_MEM_DEVICE inputs live in the caller's buffers: a solve's repair must read them in stream order,
+    so a refill the caller enqueues on the stream after wbq_solve and before reading the outputs must not
+    reach the solve (with device inputs every solve enqueues its follow-up kernel)."""
+    torch = pytest.importorskip("torch")
+    tight, _, _, heavy = cases(oracle_lib)
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(tight, heavy)
+    other = qppvm_instances(tight, 64, seed=333)
+    live = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in heavy.items()}
+    alt = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in other.items()}
+    s = wbq_mod.QPPVMSolver(tight, max_batch=64)
+    try:
+        s.set_option(s.OPT_FOLLOWUP, 1)
+        s.set_stream(torch.cuda.current_stream().cuda_stream)
+        s.set_device_inputs({k: v.data_ptr() for k, v in live.items()}, 64)
+        s.solve()
+        for k in live:  # the caller refills its buffers on the same stream
+            live[k].copy_(alt[k])
+        t1, s1, _ = s.outputs()
+    finally:
+        s.close()
+    np.testing.assert_array_equal(s1, st_r)
+    ok = st_r == 0
+    assert rel_err(t1[ok], tau_r[ok]) <= TOL

@@ -1,9 +1,7 @@
 """n > 32: the repair kernel hands an instance whose pinned level 1 needs the dual active set back to an
 active-set pass over work list 2 (qppvm_kernel.hip, qppvm_active_kernel<..., true>) instead of running the
-loop itself. Same results as the in-repair loop (WBQ_HANDBACK=0, read when a context is created) and as
+loop itself. Same results as the in-repair loop (wbq_set_option WBQ_OPT_HANDBACK = 0) and as
 the oracle (tau within 1e-6 relative, statuses equal), cold and warm, and in per-step rollouts."""
-import os
-
 import numpy as np
 import pytest
 
@@ -23,15 +21,9 @@ def wbq_mod():
 
 
 def solver(wbq_mod, prob, B, handback):
-    old = os.environ.get("WBQ_HANDBACK")
-    os.environ["WBQ_HANDBACK"] = "1" if handback else "0"
-    try:
-        return wbq_mod.QPPVMSolver(prob, max_batch=B)
-    finally:
-        if old is None:
-            del os.environ["WBQ_HANDBACK"]
-        else:
-            os.environ["WBQ_HANDBACK"] = old
+    s = wbq_mod.QPPVMSolver(prob, max_batch=B)
+    s.set_option(s.OPT_HANDBACK, 1 if handback else 0)
+    return s
 
 
 @pytest.mark.parametrize("n,tm", [(39, 30.0), (39, 80.0), (48, 40.0)])
@@ -82,19 +74,13 @@ def test_handback_per_step_rollout(wbq_mod):
 
 @pytest.mark.parametrize("handoff", [1, 3])
 def test_active_loop_handoff_to_repair(wbq_mod, oracle_lib, handoff):
-    """WBQ_GI_HANDOFF (n > 32): an active-set loop still running after `handoff` steps goes to the level-0
-    repair as if infeasible; a feasible instance comes back with no pins, so the result is the oracle's."""
+    """WBQ_OPT_GI_HANDOFF (n > 32): an active-set loop still running after `handoff` steps goes to the
+    level-0 repair as if infeasible; a feasible instance comes back with no pins, so the result is the
+    oracle's."""
     prob = QPPVMProblem(n=39, tau_max=60.0)
     inp = qppvm_instances(prob, 64, seed=1234)
-    old = os.environ.get("WBQ_GI_HANDOFF")
-    os.environ["WBQ_GI_HANDOFF"] = str(handoff)
-    try:
-        s = wbq_mod.QPPVMSolver(prob, max_batch=64)
-    finally:
-        if old is None:
-            del os.environ["WBQ_GI_HANDOFF"]
-        else:
-            os.environ["WBQ_GI_HANDOFF"] = old
+    s = wbq_mod.QPPVMSolver(prob, max_batch=64)
+    s.set_option(s.OPT_GI_HANDOFF, handoff)
     try:
         tau, st, it = s.solve_batch(inp)
     finally:
