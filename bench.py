@@ -152,7 +152,7 @@ def euler_stability(prob, inp, dt, sample=256):
 
 
 def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False, dist=False, host_io=False,
-        weight=0, global_batch=65536, plant=False):
+        weight=0, global_batch=65536, plant=False, repair_share=True):
     """Times `steps` solves; returns a dict of measurements (max over ranks when dist)."""
     import torch
     plan = shard_plan(config, B, world, global_batch)
@@ -259,7 +259,7 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
     ag_ms = float(np.mean([a.elapsed_time(b) for a, b in ag_events])) if ag_events else 0.0
     tau, status, iters = solver.outputs()
     mpc = None
-    if config == 4 and form == "qppvm":
+    if config == 4 and form == "qppvm" and repair_share:
         # repair share: one more rollout from the measured state, one step per call, reading the
         # warm-start hints (1 = that step's level 0 was infeasible: the BVLS repair ran)
         solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)
@@ -323,7 +323,10 @@ def pmc_traffic(args, form):
                    sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-pmc", "--no-variant",
                    "--steps", "20", "--warmup", "2", "--form", form, "--config", str(args.config),
                    "--batch", str(args.batch), "--global-batch", str(args.global_batch), "--n", str(args.n),
-                   "--weight", args.weight, "--mpc-inputs", args.mpc_inputs]
+                   "--weight", args.weight, "--mpc-inputs", args.mpc_inputs,
+                   # (config 4: the PMC child runs only the timed twenty-step rollout launches, not the one-step
+                   # launches of the repair-share pass, so the per-launch bytes are one launch shape's)
+                   "--no-repair-share"]
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
@@ -473,6 +476,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     ap.add_argument("--no-variant", action="store_true", help="skip the contact-form variant line")
+    ap.add_argument("--no-repair-share", action="store_true",
+                    help="config 4: skip the one-step-per-call rollout that measures the repair share (the PMC child "
+                         "uses this, so its counters see the timed launch shape only)")
     ap.add_argument("--host-io", action="store_true",
                     help="PCIe-inclusive rate: host inputs copied in and outputs copied out every step "
                          "(never the headline value; DESIGN.md reports it beside it)")
@@ -508,7 +514,7 @@ def main():
     fused = fused_rollout(args.form, args.config, weight, n, plant)
     kern = dominant_kernel(args.form, weight, fused)
     m = run(args.form, args.config, n, B, args.steps, args.warmup, world, rank, device, allgather, dist,
-            args.host_io, weight, args.global_batch, plant)
+            args.host_io, weight, args.global_batch, plant, repair_share=not args.no_repair_share)
     value = m["total"] / m["dt"]
     # algorithmic bytes of one launch of the dominant kernel: the fused rollout kernel solves the batch
     # HORIZON times (each solve stages its instance's inputs again: nothing is skipped)

@@ -136,13 +136,12 @@ struct FastLdsLayout {
     int SIZE;
     __host__ __device__ FastLdsLayout(int T, int m0)
     {
+        // (the streamed LDL^T variant's layout, NP = 32, is smaller than the merged active-set layout: checked
+        // by launch_np. Not folded in here: a further select in this expression cost the compiler the proof
+        // that every instance's LDS is 16-byte aligned, and every 16-byte LDS read fell back to ds_read2_b64 --
+        // config 1 32.4 -> 39.6 us on one box)
         const int f = FastLayout<NP>(T, m0).SIZE, g = ActiveLayout<NP>(T, m0).SIZE;
-        int s = (MERGED && g > f) ? g : f;
-        if (NP == 32 && T <= 2 && m0 <= 6) { // (the streamed LDL^T variant's layout)
-            const int l = LdlLayout(T, m0).SIZE;
-            s = l > s ? l : s;
-        }
-        SIZE = s;
+        SIZE = (MERGED && g > f) ? g : f;
     }
 };
 
@@ -727,12 +726,13 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
 // overhead of any follow-up kernel (scripts/launch_probe2.hip, launch_probe3.hip: registers, LDS,
 // scratch, kernarg size and a cold L2 do not change it); rocprofv3's ~5 us duration for it includes
 // the dispatch.
-// The fused rollout's level-0 repair behind a call (WBQ_ROLL_REPAIR_NOINLINE, default 1 since round 5): the
-// step's fast path then keeps its registers instead of spilling around the repair's (config 4, same box:
-// WRITE_SIZE per 20-step launch 730 -> 156 MB, a repair-free 4096 x 20 rollout 0.75 -> 0.51 ms, a repairing one
-// 3.25 -> 3.33 ms). Round 4's build of this faulted on MI355X; on round 5's sources it passes.
+// The fused rollout's level-0 repair behind a call (WBQ_ROLL_REPAIR_NOINLINE = 1; round 5's default): the step's
+// fast path then keeps more of its registers (round 5, same box: WRITE_SIZE per 20-step launch 730 -> 156 MB).
+// Round 4's build of this form faulted on MI355X with no repair running and the cause was not found (DESIGN.md
+// 3.5), so the default is the inlined repair again (round 6): on round 6's sources it is also the faster form
+// (config 4 24.1 -> 26.0 M QP/s, WRITE_SIZE 142 -> 245 MB per launch, same box: profiles/r06_*).
 #ifndef WBQ_ROLL_REPAIR_NOINLINE
-#define WBQ_ROLL_REPAIR_NOINLINE 1
+#define WBQ_ROLL_REPAIR_NOINLINE 0
 #endif
 template <int NP, int M0>
 __device__ __noinline__ void repair_instance_call(const QppvmArgs &a, double *S, long b, int i, bool rep)
@@ -1723,6 +1723,8 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     if (grid == 0) return hipSuccess;
     constexpr bool MERGED = NP == 32; // active-set layout fits next to the fast one
     using Lay = FastLdsLayout<NP, MERGED>;
+    if (NP == 32 && a.ntasks <= 2 && a.m0 <= 6 && LdlLayout(a.ntasks, a.m0).SIZE > Lay(a.ntasks, a.m0).SIZE)
+        return hipErrorInvalidValue; // (the streamed LDL^T path's layout must fit the instance's LDS)
     hipError_t e;
     if constexpr (NP == 32 && kInlineRepair<M0>) { // a whole rollout in one launch
         if (a.steps > 0 || a.prepare) {
