@@ -164,6 +164,8 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
                                               double nn2, bool act, double &zz)
 {
     constexpr int RS = NP + 1;
+    // (measured, round 6: the LDS reads of these dots issued a chunk ahead -- dot4p / dot4sp, wbq_device.h --
+    // spilled the n <= 32 fast kernel that inlines this loop, 0 -> ~300 B of scratch even at 4-element chunks)
     const double d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
     S[L.D1 + i] = d1;
     __syncthreads();

@@ -148,6 +148,8 @@ struct RowStore<NP, true> {
             if (j < cnt) s[j & 3] = fma(v[j], b[j], s[j & 3]);
         return (s[0] + s[1]) + (s[2] + s[3]);
     }
+    // (the full row, LDS reads a chunk ahead: rdotp below)
+    __device__ double dotp(const double *b) const;
 };
 
 template <int NP>
@@ -178,6 +180,7 @@ struct RowStore<NP, false> {
         }
         return (s[0] + s[1]) + (s[2] + s[3]);
     }
+    __device__ double dotp(const double *b) const { return dot(b, NP); }
 };
 
 // Dot product of two N-vectors (LDS or registers) with four independent accumulators: the
@@ -210,6 +213,98 @@ __device__ __forceinline__ double dot4s(const double *a, int stride, const doubl
         s3 = fma(a[(j + 3) * stride], b[j + 3], s3);
     }
     return (s0 + s1) + (s2 + s3);
+}
+
+// The same dot products with every LDS read issued a chunk (CH elements) ahead of the FMAs that use it (round
+// 6): inside the dual active-set loop, at the 256-VGPR cap, the compiler's own schedule read two elements and
+// waited (lgkmcnt(0)) before the next two -- ~16 dependent LDS round trips per dot, which set the step time of
+// the waves that run the loop long after the others have finished. Two chunks are in
+// registers at a time (4 CH doubles per operand pair; CH = 8 spilled the fast kernel that inlines the loop).
+template <int N, int CH = 4>
+__device__ __forceinline__ double dot4p(const double *a, const double *b)
+{
+    static_assert(N % CH == 0 && CH % 4 == 0, "dot4p: N, CH");
+    constexpr int NCH = N / CH;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double av[2][CH], bv[2][CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        av[0][u] = a[u];
+        bv[0][u] = b[u];
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 1 < NCH) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                av[(ch + 1) & 1][u] = a[(ch + 1) * CH + u];
+                bv[(ch + 1) & 1][u] = b[(ch + 1) * CH + u];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) s[u & 3] = fma(av[ch & 1][u], bv[ch & 1][u], s[u & 3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+// a strided (a column of a row-major LDS matrix)
+template <int N, int CH = 4>
+__device__ __forceinline__ double dot4sp(const double *a, int stride, const double *b)
+{
+    static_assert(N % CH == 0 && CH % 4 == 0, "dot4sp: N, CH");
+    constexpr int NCH = N / CH;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double av[2][CH], bv[2][CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        av[0][u] = a[u * stride];
+        bv[0][u] = b[u];
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 1 < NCH) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                av[(ch + 1) & 1][u] = a[((ch + 1) * CH + u) * stride];
+                bv[(ch + 1) & 1][u] = b[(ch + 1) * CH + u];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) s[u & 3] = fma(av[ch & 1][u], bv[ch & 1][u], s[u & 3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+// a register vector (compile-time indices) times an LDS vector
+template <int N, int CH = 4>
+__device__ __forceinline__ double rdotp(const double (&v)[N], const double *b)
+{
+    static_assert(N % CH == 0 && CH % 4 == 0, "rdotp: N, CH");
+    constexpr int NCH = N / CH;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double bv[2][CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) bv[0][u] = b[u];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 1 < NCH) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) bv[(ch + 1) & 1][u] = b[(ch + 1) * CH + u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) s[u & 3] = fma(v[ch * CH + u], bv[ch & 1][u], s[u & 3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+template <int NP>
+__device__ __forceinline__ double RowStore<NP, true>::dotp(const double *b) const
+{
+    return rdotp<NP>(v, b);
 }
 
 // ---------------------------------------------------------------- reductions inside an instance
