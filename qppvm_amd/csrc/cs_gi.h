@@ -1,0 +1,510 @@
+// cs_gi.h -- the n <= 32 dual active set carried in constraint space (round 6), two instances per
+// wave64 (lanes [0, 32) and [32, 64)), lane i <-> joint i. It replaces qppvm_kernel.hip's gi_solve at
+// the fast kernel's inline call (and in the fused rollout): same problem, same interface, same statuses.
+//
+// The problem (reference src/QPPVMPlugin.cpp:201-259, the limits :56-67):
+//   min 0.5 ||u - u_hat||^2   s.t.  G u = b0,   lo <= M u <= hi
+// from the equality-constrained optimum u0 (the fast path's u) and Q1 (an orthonormal basis of G's rows).
+// With P = I - Q1^T Q1 the dual active set only ever needs Gamma = M P M -- the Gram of the bound normals
+// projected onto null(G) -- and the activities s = M u:
+//   adding bound p (side sg_p): v = sg_A sg_p Gamma[A][p], r = K^-1 v (K = Gamma_AA signed), d2 = Gamma_pp - v.r,
+//   ds = sg_p Gamma[:][p] - Gamma[:][A] sg_A r (the change of every activity per unit step), the step
+//   t = min(t1 (a multiplier reaches zero), t2 = -slack_p / (sg_p ds_p)); s += t ds, lambda_A -= t r.
+// Gamma's columns are formed on demand, one per bound that enters the active set: w = P m_p (six DPP sums),
+// c = M w (one LDS dot against M's row in registers), kept in LDS (GA, one row per lane over the slots). K is
+// kept as T = L^-1 (K = L L^T, packed rows in LDS; an add appends one row in closed form, a drop re-appends the
+// rows after it, as dual_gi.h). Per pass that is O(k) LDS reads per lane plus one 32-element dot, where the
+// u-space loop it replaces (T rows and M rows in VGPRs, Gram-Schmidt against Q1 in LDS) read four 32-element
+// dots per pass at the 256-VGPR cap, each LDS read waited for in turn (DESIGN.md 3.1, round 5 lap counters:
+// ~20k cycles per select pass, ~46k per full pass, ~123k for the config-2 warm batch).
+// The incremental activities drift from the exact ones by roundoff, so when no bound is violated u is rebuilt
+// from the multipliers, u = u0 + P M rho (rho_j = sg lambda on the active joints), x = M u, with refinement
+// passes on the active set (lambda += K^-1 (beta_A - sg_A x_A)), and every bound re-checked at the exact x.
+// What the storage or the numerics cannot carry (more than KM active bounds, an active bound the rebuilt x
+// misses, the rebuild-round cap) is handed to the level-0 repair as if level 0 were infeasible: its BVLS
+// settles level 0 first and a feasible instance comes back unpinned to the u-space loop -- the same solution
+// by another path (as the n > 32 hand-off).
+// The numpy statement of this loop, step for step: scripts/emulate_cs_gi.py.
+#pragma once
+#include "wbq_kernels.h"
+#include "wbq_device.h"
+
+namespace wbq {
+
+// Per-instance LDS (doubles), inside ActiveLayout<32>'s 1,248 (the caller's Q1 rows at the start of the
+// region are read into registers first; GA then overlays them)
+struct CsLayout {
+    static constexpr int NP = 32, KM = 24, GS = KM + 1; // slots; GA row stride (odd: lane rows conflict-free)
+    static constexpr int GA = 0;                        // [NP][GS] Gamma[i][act_a]
+    static constexpr int TP = GA + NP * GS;             // T = L^-1, packed lower rows, KM (KM + 1) / 2
+    static constexpr int WV = TP + KM * (KM + 1) / 2;   // w = P m_p, then u (broadcast vectors)
+    static constexpr int VV = WV + NP;                  // v, residuals, rho by joint
+    static constexpr int LV = VV + NP;                  // l = T v
+    static constexpr int RV = LV + NP;                  // sg r
+    static constexpr int SIZE = RV + NP;
+};
+static_assert(CsLayout::SIZE <= 32 * 33 + 6 * 32, "CsLayout fits ActiveLayout<32>");
+static_assert(CsLayout::WV % 2 == 0 && CsLayout::TP % 2 == 0, "16-byte aligned vectors");
+
+// ---------------------------------------------------------------- NP = 32 lane helpers
+// value of v at lane idx of this lane's instance (idx instance-uniform): two v_readlane, no LDS
+__device__ __forceinline__ double cs_bcast(double v, int idx)
+{
+    const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
+    const double a0 = lane_f64(v, i0), a1 = lane_f64(v, 32 + i1);
+    return (threadIdx.x & 32) ? a1 : a0;
+}
+__device__ __forceinline__ int cs_bcast_i(int v, int idx)
+{
+    const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
+    const int a0 = __builtin_amdgcn_readlane(v, i0), a1 = __builtin_amdgcn_readlane(v, 32 + i1);
+    return (threadIdx.x & 32) ? a1 : a0;
+}
+// value at lane s of each instance (s wave-uniform)
+__device__ __forceinline__ double cs_at(double v, int s)
+{
+    const double a0 = lane_f64(v, s), a1 = lane_f64(v, 32 + s);
+    return (threadIdx.x & 32) ? a1 : a0;
+}
+// wave-uniform max / min of an instance-uniform count (SGPR: loops over it are scalar loops)
+__device__ __forceinline__ int cs_wmax(int v)
+{
+    const int a0 = __builtin_amdgcn_readlane(v, 0), a1 = __builtin_amdgcn_readlane(v, 32);
+    return a0 > a1 ? a0 : a1;
+}
+__device__ __forceinline__ int cs_wmin(int v)
+{
+    const int a0 = __builtin_amdgcn_readlane(v, 0), a1 = __builtin_amdgcn_readlane(v, 32);
+    return a0 < a1 ? a0 : a1;
+}
+
+// M's row (in registers) times a 32-vector in LDS: every read issued before the first FMA (one LDS round trip)
+__device__ __forceinline__ double cs_rdot(const double (&m)[32], const double *b)
+{
+    double bv[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) bv[j] = b[j];
+    __builtin_amdgcn_sched_barrier(0);
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 32; ++j) s[j & 3] = fma(m[j], bv[j], s[j & 3]);
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+// sum_{j < cnt} row[j] vec[j] over the slots (row: this lane's LDS row, vec: a broadcast LDS vector), chunks
+// of eight reads issued together; kmax (wave-uniform, >= cnt, <= KM) bounds the scalar loop
+__device__ __forceinline__ double cs_sdot(const double *row, const double *vec, int cnt, int kmax)
+{
+    double s0 = 0.0, s1 = 0.0;
+    for (int j0 = 0; j0 < kmax; j0 += 8) {
+        double rv[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = row[j0 + u];
+            bv[u] = vec[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 = fma(j0 + u < cnt ? rv[u] : 0.0, j0 + u < cnt ? bv[u] : 0.0, s0);
+            s1 = fma(j0 + u + 1 < cnt ? rv[u + 1] : 0.0, j0 + u + 1 < cnt ? bv[u + 1] : 0.0, s1);
+        }
+    }
+    return s0 + s1;
+}
+// sum_{a <= j < cnt} T[j][a] vec[j]: column a of the packed T
+__device__ __forceinline__ double cs_tcol(const double *tp, int a, const double *vec, int cnt, int kmax)
+{
+    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
+    double s0 = 0.0, s1 = 0.0;
+    for (int j0 = 0; j0 < kmax; j0 += 8) {
+        double tv[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u < CsLayout::KM ? j0 + u : CsLayout::KM - 1;
+            tv[u] = tp[j * (j + 1) / 2 + ac];
+            bv[u] = vec[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            const bool o0 = j0 + u >= a && j0 + u < cnt, o1 = j0 + u + 1 >= a && j0 + u + 1 < cnt;
+            s0 = fma(o0 ? tv[u] : 0.0, o0 ? bv[u] : 0.0, s0);
+            s1 = fma(o1 ? tv[u + 1] : 0.0, o1 ? bv[u + 1] : 0.0, s1);
+        }
+    }
+    return s0 + s1;
+}
+__device__ __forceinline__ const double *cs_trow(const double *tp, int a)
+{
+    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
+    return tp + ac * (ac + 1) / 2;
+}
+
+// Lane state of the loop. Slot a (lane a < k): act (its joint), sg (normal = sg * M row act), lam, beta (the
+// bound in the signed form sg s_act >= beta), aeq (lo == hi: never dropped). Lane j (joint j): onact.
+struct CsSlots {
+    int k = 0, act = 0;
+    double sg = 1.0, lam = 0.0, beta = 0.0;
+    bool aeq = false;
+};
+
+// Gamma[:][p] for the instance-uniform joint p: w = P m_p, c_i = M_i . w; cpp = |w|^2 = Gamma_pp
+template <int M0>
+__device__ __forceinline__ double cs_column(double *S, const double (&mrow)[32], const double (&q1)[M0], int i,
+                                           int p, double &cpp)
+{
+    double mp = 0.0;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) mp = (r == p) ? mrow[r] : mp; // M[i][p] = M[p][i]
+    double vq[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) vq[c] = q1[c] * mp;
+    isum_vec<32, M0>(vq); // Q1 m_p
+    double w = mp;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) w = fma(-q1[c], vq[c], w);
+    cpp = isum<32>(w * w);
+    lds_barrier(); // (the previous readers of WV)
+    S[CsLayout::WV + i] = w;
+    lds_barrier();
+    return cs_rdot(mrow, S + CsLayout::WV);
+}
+
+// l = T v, r = T^T l on the slot lanes (a < cnt; v on those lanes), through VV / LV
+__device__ __forceinline__ void cs_tsolve(double *S, int i, double v, int cnt, int kmax, double &l, double &r)
+{
+    S[CsLayout::VV + i] = i < cnt ? v : 0.0;
+    lds_barrier();
+    l = i < cnt ? cs_sdot(cs_trow(S + CsLayout::TP, i), S + CsLayout::VV, i + 1, kmax) : 0.0;
+    S[CsLayout::LV + i] = l;
+    lds_barrier();
+    r = i < cnt ? cs_tcol(S + CsLayout::TP, i, S + CsLayout::LV, cnt, kmax) : 0.0;
+}
+
+// u = u0 + P M rho, x = M u on the lanes with on set (instance-uniform); collective
+template <int M0>
+__device__ __forceinline__ void cs_rebuild(double *S, const double (&mrow)[32], const double (&q1)[M0], int i,
+                                           bool on, const CsSlots &g, double u0, double &u, double &x)
+{
+    lds_barrier();
+    S[CsLayout::VV + i] = 0.0;
+    lds_barrier();
+    if (on && i < g.k) S[CsLayout::VV + g.act] = g.sg * g.lam;
+    lds_barrier();
+    const double y = cs_rdot(mrow, S + CsLayout::VV);
+    double vq[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) vq[c] = q1[c] * y;
+    isum_vec<32, M0>(vq);
+    double py = y;
+#pragma unroll
+    for (int c = 0; c < M0; ++c) py = fma(-q1[c], vq[c], py);
+    const double un = u0 + py;
+    S[CsLayout::WV + i] = un;
+    lds_barrier();
+    const double xn = cs_rdot(mrow, S + CsLayout::WV);
+    if (on) {
+        u = un;
+        x = xn;
+    }
+}
+
+constexpr int kCsRounds = 8;       // rebuilds per solve before the hand-off
+constexpr double kCsDep = 1e-14;   // a row whose Schur complement is below kCsDep Gamma_pp is dependent
+
+// The loop (see the head of this file). Q1's rows are in S's first rows (stride 33, the active-set layout's
+// QA) on entry. Returns this lane's x = M u (exact, rebuilt); u_out = u. status 1: step cap; infeasible: no
+// step exists (level 0 not attainable at b0 inside the bounds) or the hand-off described above. wsg: the
+// warm side of this lane's bound (+1 lower, -1 upper, 0 none); record: the final active set to ws_rows.
+template <int M0>
+__device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
+                                           double lo, double hi, double u0, int &status, int &iters,
+                                           bool &infeasible, int wsg, bool record, double &u_out)
+{
+    using L = CsLayout;
+    constexpr int KM = L::KM, GS = L::GS;
+    const int n = a.n, m0 = a.m0;
+    const int ic = i < n ? i : n - 1;
+    double q1[M0];
+#pragma unroll
+    for (int c = 0; c < M0; ++c) q1[c] = c < m0 ? S[c * 33 + i] : 0.0;
+    const double *Mb = a.M + b * n * n + ic;
+    double mrow[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) mrow[r] = Mb[(r < n ? r : n - 1) * n];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
+    double nrm2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) nrm2 = fma(mrow[r], mrow[r], nrm2);
+    const double nrm = sqrt(nrm2);
+    int dim;
+    {
+        double qq[M0];
+#pragma unroll
+        for (int c = 0; c < M0; ++c) qq[c] = q1[c] * q1[c];
+        isum_vec<32, M0>(qq);
+        int rk = 0;
+#pragma unroll
+        for (int c = 0; c < M0; ++c) rk += (c < m0 && qq[c] > 0.5) ? 1 : 0;
+        dim = n - rk; // independent bound normals the loop can hold (rank cap)
+    }
+    const bool eqb = lo == hi;
+    lds_barrier(); // every lane has its Q1 column: the region is the loop's now
+    S[L::WV + i] = u0;
+    lds_barrier();
+    double s = cs_rdot(mrow, S + L::WV); // s = M u0
+    double u = u0, x = s;
+    CsSlots g;
+    bool onact = false;
+    infeasible = false;
+    bool dirty = false;
+    // ------------------------------------------------ warm start: the last active set in one batch
+    if (__any(go && row && wsg != 0)) {
+        const bool wme = go && row && wsg != 0;
+        const unsigned long long bal = __ballot(wme);
+        unsigned rem = (unsigned)(bal >> (threadIdx.x & 32));
+        const int kw = __popc(rem);
+        const int kwmax = cs_wmax(kw);
+        bool dep = kw > KM || kw > dim;
+        for (int a2 = 0; a2 < kwmax; ++a2) {
+            const bool on = a2 < kw && !dep;
+            const int j = rem ? __builtin_ctz(rem) : 0;
+            rem &= rem ? rem - 1u : 0u;
+            const double sj = (double)cs_bcast_i(wsg, j);
+            double cpp;
+            const double c = cs_column<M0>(S, mrow, q1, i, j, cpp);
+            const double cg = __shfl(c, g.act, 32);
+            const double v = (on && i < a2) ? g.sg * sj * cg : 0.0;
+            double l, r;
+            cs_tsolve(S, i, v, on ? a2 : 0, a2 < KM ? a2 + 1 : KM, l, r);
+            const double d2 = cpp - isum<32>(l * l);
+            if (on && !(d2 > kCsDep * cpp)) dep = true; // a dependent batch: start cold
+            const bool on2 = on && !dep;
+            const double id = d2 > 0.0 ? frsq(d2) : 0.0;
+            if (on2 && i < a2) S[L::TP + a2 * (a2 + 1) / 2 + i] = -r * id;
+            if (on2 && i == a2) S[L::TP + a2 * (a2 + 1) / 2 + a2] = id;
+            if (on2) S[L::GA + i * GS + a2] = c;
+            const double loj = cs_bcast(lo, j), hij = cs_bcast(hi, j);
+            const bool eqj = cs_bcast_i(eqb ? 1 : 0, j) != 0;
+            if (on2 && i == a2) {
+                g.act = j;
+                g.sg = sj;
+                g.lam = 0.0;
+                g.aeq = eqj;
+                g.beta = sj > 0.0 ? loj : -hij;
+            }
+        }
+        // multipliers of the batch optimum from u0: K lambda = beta_W - sg_W s_W
+        const int kk = dep ? 0 : kw;
+        const double xa = __shfl(s, g.act, 32);
+        double l, lw;
+        cs_tsolve(S, i, g.beta - g.sg * xa, kk, kwmax < KM ? kwmax : KM, l, lw);
+        const double lmx = imax<32>(i < kk ? fabs(lw) : 0.0);
+        const bool bad = imax<32>((i < kk && !g.aeq && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
+        const bool keep = kk > 0 && !bad;
+        S[L::RV + i] = (keep && i < kk) ? g.sg * lw : 0.0;
+        lds_barrier();
+        const double dsw = cs_sdot(S + L::GA + i * GS, S + L::RV, keep ? kk : 0, kwmax < KM ? kwmax : KM);
+        if (keep) {
+            s += dsw;
+            if (i < kk) g.lam = g.aeq ? lw : fmax(lw, 0.0);
+            g.k = kk;
+            onact = wme;
+            iters += 1;
+            dirty = true;
+        }
+    }
+    // ------------------------------------------------ the loop
+    const int maxit = a.max_iter;
+    bool need_select = true, recheck = false, have_col = false;
+    int rounds = 0, p = 0, cdrop = -1;
+    double sgp = 1.0, bnd = 0.0, lamp = 0.0, c = 0.0, cpp = 0.0;
+    bool peq = false;
+    while (true) {
+        if (__any(cdrop >= 0)) {
+            // drop slot cdrop: the slots after it move down; T rows before it stand, the later ones are
+            // re-appended from their Gamma columns (GA)
+            const bool dr = cdrop >= 0;
+            const int cd = dr ? cdrop : 0;
+            const int cb = cs_bcast_i(g.act, cd);
+            if (dr && i == cb) onact = false;
+            const int na = __shfl(g.act, i + 1, 32);
+            const double ns = __shfl(g.sg, i + 1, 32), nl = __shfl(g.lam, i + 1, 32), nb = __shfl(g.beta, i + 1, 32);
+            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1, 32) != 0;
+            if (dr && i >= cd) {
+                g.act = na;
+                g.sg = ns;
+                g.lam = nl;
+                g.beta = nb;
+                g.aeq = ne;
+            }
+            if (dr) {
+                for (int a3 = cd; a3 + 1 < g.k; ++a3) S[L::GA + i * GS + a3] = S[L::GA + i * GS + a3 + 1];
+                --g.k;
+            }
+            lds_barrier();
+            const int amin = cs_wmin(dr ? cd : KM), amax = cs_wmax(dr ? g.k : 0);
+            for (int a2 = amin; a2 < amax; ++a2) {
+                const bool on = dr && a2 >= cd && a2 < g.k;
+                const double sa = cs_at(g.sg, a2);
+                const double gv = S[L::GA + g.act * GS + a2]; // Gamma[act_b][act_a2]
+                const double diag = cs_at(gv, a2);
+                double l, r;
+                cs_tsolve(S, i, sa * g.sg * gv, on ? a2 : 0, a2 + 1, l, r);
+                const double e2 = diag - isum<32>(l * l);
+                const double id = e2 > 0.0 ? frsq(e2) : 0.0;
+                if (on && i < a2) S[L::TP + a2 * (a2 + 1) / 2 + i] = -r * id;
+                if (on && i == a2) S[L::TP + a2 * (a2 + 1) / 2 + a2] = id;
+            }
+            cdrop = -1;
+            lds_barrier();
+        }
+        bool rb = false;
+        if (need_select) {
+            double v = -1.0;
+            if (go && row && !onact) {
+                const double tol = 1e-10 * fmax(1.0, fmax(fabs(s), fmax(fabs(lo), fabs(hi))));
+                const double viol = fmax(lo - s, s - hi);
+                if (viol > tol) v = viol / nrm;
+            }
+            int pi = i;
+            iargmax<32>(v, pi);
+            if (!(v > 0.0) || recheck) {
+                recheck = false;
+                // no violated bound at these activities: optimal if they are exact, else rebuild first
+                rb = go && dirty;
+                if (go && !dirty) go = false;
+            } else {
+                p = pi;
+                sgp = (cs_bcast(lo - s, p) > cs_bcast(s - hi, p)) ? 1.0 : -1.0;
+                bnd = sgp > 0.0 ? cs_bcast(lo, p) : cs_bcast(hi, p);
+                peq = cs_bcast_i(eqb ? 1 : 0, p) != 0;
+                lamp = 0.0;
+                have_col = false;
+            }
+        }
+        if (__any(rb)) {
+            // u and x from the multipliers, refinement on the active set, then every bound re-checked
+            cs_rebuild<M0>(S, mrow, q1, i, rb, g, u0, u, x);
+            const int kmx = cs_wmax(rb ? g.k : 0);
+            if (kmx > 0) {
+                for (int pass = 0; pass < 3; ++pass) {
+                    const double xa = __shfl(x, g.act, 32);
+                    const double res = (rb && i < g.k) ? g.beta - g.sg * xa : 0.0;
+                    const double rmx = imax<32>(rb ? fabs(res) / (1.0 + fabs(xa)) : 0.0);
+                    if (!__any(rb && rmx > 1e-13)) break;
+                    double l, dl;
+                    cs_tsolve(S, i, res, rb ? g.k : 0, kmx, l, dl);
+                    if (rb && i < g.k) g.lam += dl;
+                    cs_rebuild<M0>(S, mrow, q1, i, rb, g, u0, u, x);
+                }
+                // every active bound must hold at the rebuilt x, else the factor is too poor: hand off
+                const double xa = __shfl(x, g.act, 32);
+                const double miss = (rb && i < g.k) ? fabs(g.beta - g.sg * xa) / (1.0 + fabs(xa)) : 0.0;
+                if (rb && imax<32>(miss) > 1e-8) {
+                    infeasible = true;
+                    go = false;
+                }
+            }
+            if (rb) {
+                s = x;
+                dirty = false;
+                if (++rounds > kCsRounds && go) {
+                    infeasible = true;
+                    go = false;
+                }
+            }
+            continue;
+        }
+        if (!__any(go)) break;
+        if (__any(go && !have_col)) { // (a drop keeps stepping on p: its column is kept)
+            double cppn;
+            const double cn = cs_column<M0>(S, mrow, q1, i, p, cppn);
+            if (!have_col) {
+                c = cn;
+                cpp = cppn;
+                have_col = true;
+            }
+        }
+        // ---- the step for bound p
+        const int k = g.k, kmx = cs_wmax(go ? k : 0);
+        const double cg = __shfl(c, g.act, 32); // Gamma[act_a][p] on slot lane a
+        const double v = (i < k) ? g.sg * sgp * cg : 0.0;
+        double l, r;
+        cs_tsolve(S, i, v, go ? k : 0, kmx, l, r);
+        const double d2 = cpp - isum<32>(l * l);
+        S[L::RV + i] = (go && i < k) ? g.sg * r : 0.0;
+        lds_barrier();
+        const double ds = sgp * c - cs_sdot(S + L::GA + i * GS, S + L::RV, go ? k : 0, kmx);
+        const double zz = sgp * cs_bcast(ds, p);
+        const double slack = sgp * (cs_bcast(s, p) - bnd); // < 0: violated
+        const double rmax = imax<32>(i < k ? fabs(r) : 0.0);
+        double cand = (i < k && !g.aeq && r > 1e-13 * rmax) ? g.lam / r : kInf;
+        int ci = i;
+        iargmin<32>(cand, ci);
+        const double t1 = cand;
+        const double t2 = (k < dim && d2 > kCsDep * cpp && zz > 0.0) ? -slack / zz : kInf;
+        if (go) {
+            if (t1 >= kInf && t2 >= kInf) {
+                // no step: the bounds cannot all be met -- unless the incremental activities drifted; then
+                // rebuild, re-check, select again, and report it only if the exact activities agree
+                if (dirty) {
+                    recheck = true;
+                    need_select = true;
+                } else {
+                    infeasible = true;
+                    go = false;
+                }
+            } else if (t2 <= t1 && k >= KM) {
+                infeasible = true; // slot storage: hand off
+                go = false;
+            } else {
+                dirty = true;
+                const double t = fmin(t1, t2);
+                s = fma(t, ds, s);
+                if (i < k) g.lam = fma(-t, r, g.lam);
+                lamp += t;
+                ++iters;
+                if (t2 <= t1) { // add p: T row k = [-r^T / d, 1 / d], Gamma column k = c
+                    const double id = frsq(d2);
+                    if (i < k) S[L::TP + k * (k + 1) / 2 + i] = -r * id;
+                    if (i == k) {
+                        S[L::TP + k * (k + 1) / 2 + k] = id;
+                        g.act = p;
+                        g.sg = sgp;
+                        g.lam = lamp;
+                        g.aeq = peq;
+                        g.beta = sgp > 0.0 ? bnd : -bnd;
+                    }
+                    S[L::GA + i * GS + k] = c;
+                    if (i == p) onact = true;
+                    ++g.k;
+                    need_select = true;
+                } else { // drop slot ci (its multiplier reached zero), keep stepping on p
+                    cdrop = ci;
+                    need_select = false;
+                }
+                if (iters >= maxit && go) {
+                    status = 1;
+                    go = false;
+                }
+            }
+        }
+        lds_barrier();
+    }
+    if (record) { // the final active set, by joint, for the next solve of this instance
+        lds_barrier();
+        S[L::VV + i] = 0.0;
+        lds_barrier();
+        if (i < g.k && !g.aeq) S[L::VV + g.act] = g.sg;
+        lds_barrier();
+        const double sgn = S[L::VV + i];
+        const bool ok = status == 0 && !infeasible;
+        if (row && a.ws_rows) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
+        lds_barrier();
+    }
+    u_out = u;
+    return x;
+}
+
+}  // namespace wbq

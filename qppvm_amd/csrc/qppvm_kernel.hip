@@ -37,6 +37,7 @@
 #include "wbq_kernels.h"
 #include "wbq_device.h"
 #include "qppvm_repair.h"
+#include "cs_gi.h"
 
 #include <math.h>
 #include <type_traits>
@@ -68,6 +69,11 @@
 // Gauss-Jordan path (rounds 1-5), for A/B builds
 #ifndef WBQ_FAST_LDL
 #define WBQ_FAST_LDL 1
+#endif
+// Round 6: the n <= 32 inline dual active set carried in constraint space (cs_gi.h: Gamma = M P M columns on
+// demand, T = L^-1 of the active Gram in LDS); 0: the u-space loop of rounds 1-5 (gi_solve), for A/B builds
+#ifndef WBQ_GI_CS
+#define WBQ_GI_CS 1
 #endif
 // dual active set, n > 32 (T rows in LDS): a dropped bound leaves the basis by Givens rotations (1) or by
 // re-projecting the later active normals (0, rounds 1-4; always for n <= 32)
@@ -1581,8 +1587,13 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             bool inf = false;
             const int wsg = (ga && warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
             WBQ_STAMP(18); // (diagnostic build: the inline dual active set starts)
-            const double x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg,
-                                               true);
+            double x2, u2;
+            if constexpr (NP == 32 && WBQ_GI_CS != 0) {
+                x2 = cs_solve<M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2);
+            } else {
+                x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true);
+                u2 = S[LA.U + i];
+            }
             WBQ_STAMP(19);
             const bool rep = active && (inf || to_rep);
             if (active && !rep) { // (before the repair below, which reuses the wave's LDS)
@@ -1590,7 +1601,7 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
                 if (!isfinite(tau2) && st2 == 0) st2 = 3;
                 if (st2 != 0) tau2 = h_i;
                 if (row) a.tau[bn + i] = tau2;
-                rollout_step(a, b, i, row, S[LA.U + i], st2 == 0);
+                rollout_step(a, b, i, row, u2, st2 == 0);
                 if (i == 0) {
                     a.status[b] = st2;
                     a.iters[b] = it2;
