@@ -209,8 +209,11 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
             c = churn["calls"]
             lo = (c % 5) * churn["slice"]
             src = churn["alt"][1 - (c // 5) % 2]  # pool states, then the originals, ...
-            for k, t in churn["live"].items():
-                t[lo:lo + churn["slice"]].copy_(src[k][lo:lo + churn["slice"]])
+            # every field's rows in one multi-tensor copy launch (the same bytes as one copy per field, whose ten
+            # launches took ~30 us of a ~150 us step on MI355X: profiles/r06_v4_ab_*_c2.log step vs kernel)
+            sl = churn["slice"]
+            keys = list(churn["live"].keys())
+            torch._foreach_copy_([churn["live"][k][lo:lo + sl] for k in keys], [src[k][lo:lo + sl] for k in keys])
             churn["calls"] = c + 1
         if config == 4:
             solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)

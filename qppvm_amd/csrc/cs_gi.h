@@ -46,6 +46,24 @@ struct CsLayout {
 static_assert(CsLayout::SIZE <= 32 * 33 + 6 * 32, "CsLayout fits ActiveLayout<32>");
 static_assert(CsLayout::WV % 2 == 0 && CsLayout::TP % 2 == 0, "16-byte aligned vectors");
 
+// LDS ordering inside the loop. The fast kernel's workgroup is one wave, and the LDS unit executes one wave's
+// DS instructions in issue order, so a write by one lane is seen by a later read of another lane of the same
+// wave without a workgroup barrier: only the compiler must keep the order (a signal fence). lds_barrier() drains
+// every outstanding LDS access first (s_waitcnt lgkmcnt(0)): one LDS round trip per use, ~6 per pass.
+// WBQ_CS_WAVE_LDS = 0: lds_barrier() (A/B).
+#ifndef WBQ_CS_WAVE_LDS
+#define WBQ_CS_WAVE_LDS 1
+#endif
+__device__ __forceinline__ void cs_order()
+{
+#if WBQ_CS_WAVE_LDS
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    lds_barrier();
+#endif
+}
+
 // ---------------------------------------------------------------- NP = 32 lane helpers
 // value of v at lane idx of this lane's instance (idx instance-uniform): two v_readlane, no LDS
 __device__ __forceinline__ double cs_bcast(double v, int idx)
@@ -91,9 +109,10 @@ __device__ __forceinline__ double cs_rdot(const double (&m)[32], const double *b
     return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
-// sum_{j < cnt} row[j] vec[j] over the slots (row: this lane's LDS row, vec: a broadcast LDS vector), chunks
-// of eight reads issued together; kmax (wave-uniform, >= cnt, <= KM) bounds the scalar loop
-__device__ __forceinline__ double cs_sdot(const double *row, const double *vec, int cnt, int kmax)
+// sum_j row[j] vec[j] over the slots j < kmax (row: this lane's GA row, finite everywhere -- zeroed at the
+// start; vec: a broadcast LDS vector, zero past the live slots, so no masks), chunks of eight reads issued
+// together; kmax (wave-uniform, <= KM) bounds the scalar loop
+__device__ __forceinline__ double cs_gdot(const double *row, const double *vec, int kmax)
 {
     double s0 = 0.0, s1 = 0.0;
     for (int j0 = 0; j0 < kmax; j0 += 8) {
@@ -105,14 +124,37 @@ __device__ __forceinline__ double cs_sdot(const double *row, const double *vec, 
         }
 #pragma unroll
         for (int u = 0; u < 8; u += 2) {
-            s0 = fma(j0 + u < cnt ? rv[u] : 0.0, j0 + u < cnt ? bv[u] : 0.0, s0);
-            s1 = fma(j0 + u + 1 < cnt ? rv[u + 1] : 0.0, j0 + u + 1 < cnt ? bv[u + 1] : 0.0, s1);
+            s0 = fma(rv[u], bv[u], s0);
+            s1 = fma(rv[u + 1], bv[u + 1], s1);
         }
     }
     return s0 + s1;
 }
-// sum_{a <= j < cnt} T[j][a] vec[j]: column a of the packed T
-__device__ __forceinline__ double cs_tcol(const double *tp, int a, const double *vec, int cnt, int kmax)
+// sum_{j <= a} T[a][j] vec[j]: row a of the packed T (entries past the diagonal belong to later rows: masked;
+// vec is zero past the live slots)
+__device__ __forceinline__ double cs_trowdot(const double *tp, int a, const double *vec, int kmax)
+{
+    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
+    const double *row = tp + ac * (ac + 1) / 2;
+    double s0 = 0.0, s1 = 0.0;
+    for (int j0 = 0; j0 < kmax; j0 += 8) {
+        double rv[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = row[j0 + u];
+            bv[u] = vec[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 = fma(j0 + u <= a ? rv[u] : 0.0, bv[u], s0);
+            s1 = fma(j0 + u + 1 <= a ? rv[u + 1] : 0.0, bv[u + 1], s1);
+        }
+    }
+    return s0 + s1;
+}
+// sum_{j >= a} T[j][a] vec[j]: column a of the packed T (T finite everywhere -- zeroed at the start; vec zero
+// past the live slots)
+__device__ __forceinline__ double cs_tcol(const double *tp, int a, const double *vec, int kmax)
 {
     const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
     double s0 = 0.0, s1 = 0.0;
@@ -126,17 +168,11 @@ __device__ __forceinline__ double cs_tcol(const double *tp, int a, const double 
         }
 #pragma unroll
         for (int u = 0; u < 8; u += 2) {
-            const bool o0 = j0 + u >= a && j0 + u < cnt, o1 = j0 + u + 1 >= a && j0 + u + 1 < cnt;
-            s0 = fma(o0 ? tv[u] : 0.0, o0 ? bv[u] : 0.0, s0);
-            s1 = fma(o1 ? tv[u + 1] : 0.0, o1 ? bv[u + 1] : 0.0, s1);
+            s0 = fma(j0 + u >= a ? tv[u] : 0.0, bv[u], s0);
+            s1 = fma(j0 + u + 1 >= a ? tv[u + 1] : 0.0, bv[u + 1], s1);
         }
     }
     return s0 + s1;
-}
-__device__ __forceinline__ const double *cs_trow(const double *tp, int a)
-{
-    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
-    return tp + ac * (ac + 1) / 2;
 }
 
 // Lane state of the loop. Slot a (lane a < k): act (its joint), sg (normal = sg * M row act), lam, beta (the
@@ -147,25 +183,24 @@ struct CsSlots {
     bool aeq = false;
 };
 
-// Gamma[:][p] for the instance-uniform joint p: w = P m_p, c_i = M_i . w; cpp = |w|^2 = Gamma_pp
+// Gamma[:][p] for the instance-uniform joint p: w = P m_p, c_i = M_i . w; cpp = |w|^2 = Gamma_pp. vcol: this
+// lane's column of V = Q1 M, so Q1 m_p is lane p's (no reduction)
 template <int M0>
-__device__ __forceinline__ double cs_column(double *S, const double (&mrow)[32], const double (&q1)[M0], int i,
-                                           int p, double &cpp)
+__device__ __forceinline__ double cs_column(double *S, const double (&mrow)[32], const double (&q1)[M0],
+                                           const double (&vcol)[M0], int i, int p, double &cpp)
 {
+    // M[i][p] = M[p][i] (a select chain: a select tree on p's bits became a dynamically indexed copy of the row
+    // in scratch, 0 -> 496 B)
     double mp = 0.0;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) mp = (r == p) ? mrow[r] : mp; // M[i][p] = M[p][i]
-    double vq[M0];
-#pragma unroll
-    for (int c = 0; c < M0; ++c) vq[c] = q1[c] * mp;
-    isum_vec<32, M0>(vq); // Q1 m_p
+    for (int r = 0; r < 32; ++r) mp = (r == p) ? mrow[r] : mp;
     double w = mp;
 #pragma unroll
-    for (int c = 0; c < M0; ++c) w = fma(-q1[c], vq[c], w);
+    for (int c = 0; c < M0; ++c) w = fma(-q1[c], cs_bcast(vcol[c], p), w);
     cpp = isum<32>(w * w);
-    lds_barrier(); // (the previous readers of WV)
+    cs_order(); // (the previous readers of WV)
     S[CsLayout::WV + i] = w;
-    lds_barrier();
+    cs_order();
     return cs_rdot(mrow, S + CsLayout::WV);
 }
 
@@ -173,11 +208,11 @@ __device__ __forceinline__ double cs_column(double *S, const double (&mrow)[32],
 __device__ __forceinline__ void cs_tsolve(double *S, int i, double v, int cnt, int kmax, double &l, double &r)
 {
     S[CsLayout::VV + i] = i < cnt ? v : 0.0;
-    lds_barrier();
-    l = i < cnt ? cs_sdot(cs_trow(S + CsLayout::TP, i), S + CsLayout::VV, i + 1, kmax) : 0.0;
+    cs_order();
+    l = i < cnt ? cs_trowdot(S + CsLayout::TP, i, S + CsLayout::VV, kmax) : 0.0;
     S[CsLayout::LV + i] = l;
-    lds_barrier();
-    r = i < cnt ? cs_tcol(S + CsLayout::TP, i, S + CsLayout::LV, cnt, kmax) : 0.0;
+    cs_order();
+    r = i < cnt ? cs_tcol(S + CsLayout::TP, i, S + CsLayout::LV, kmax) : 0.0;
 }
 
 // u = u0 + P M rho, x = M u on the lanes with on set (instance-uniform); collective
@@ -185,11 +220,11 @@ template <int M0>
 __device__ __forceinline__ void cs_rebuild(double *S, const double (&mrow)[32], const double (&q1)[M0], int i,
                                            bool on, const CsSlots &g, double u0, double &u, double &x)
 {
-    lds_barrier();
+    cs_order();
     S[CsLayout::VV + i] = 0.0;
-    lds_barrier();
+    cs_order();
     if (on && i < g.k) S[CsLayout::VV + g.act] = g.sg * g.lam;
-    lds_barrier();
+    cs_order();
     const double y = cs_rdot(mrow, S + CsLayout::VV);
     double vq[M0];
 #pragma unroll
@@ -200,7 +235,7 @@ __device__ __forceinline__ void cs_rebuild(double *S, const double (&mrow)[32], 
     for (int c = 0; c < M0; ++c) py = fma(-q1[c], vq[c], py);
     const double un = u0 + py;
     S[CsLayout::WV + i] = un;
-    lds_barrier();
+    cs_order();
     const double xn = cs_rdot(mrow, S + CsLayout::WV);
     if (on) {
         u = un;
@@ -212,18 +247,22 @@ constexpr int kCsRounds = 8;       // rebuilds per solve before the hand-off
 constexpr double kCsDep = 1e-14;   // a row whose Schur complement is below kCsDep Gamma_pp is dependent
 
 // The loop (see the head of this file). Q1's rows are in S's first rows (stride 33, the active-set layout's
-// QA) on entry. Returns this lane's x = M u (exact, rebuilt); u_out = u. status 1: step cap; infeasible: no
+// QA) on entry; vcol = this lane's column of V = Q1 M (the fast path has it from Y = M G^T: V^T = Y L^-T). Returns this lane's x = M u (exact, rebuilt); u_out = u. status 1: step cap; infeasible: no
 // step exists (level 0 not attainable at b0 inside the bounds) or the hand-off described above. wsg: the
 // warm side of this lane's bound (+1 lower, -1 upper, 0 none); record: the final active set to ws_rows.
-template <int M0>
+// (LAPB / LAPC: stamp slots of the diagnostic build's lap counters, as gi_solve: 8 phases from LAPB -- setup,
+// warm appends, warm multipliers, select, column, step, drop, rebuild -- and 2 counts from LAPC: passes, rebuilds)
+template <int M0, int LAPB = 0, int LAPC = 0>
 __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u0, int &status, int &iters,
-                                           bool &infeasible, int wsg, bool record, double &u_out)
+                                           bool &infeasible, int wsg, bool record, double &u_out,
+                                           const double (&vcol)[M0])
 {
     using L = CsLayout;
     constexpr int KM = L::KM, GS = L::GS;
     const int n = a.n, m0 = a.m0;
     const int ic = i < n ? i : n - 1;
+    WBQ_LAP_INIT;
     double q1[M0];
 #pragma unroll
     for (int c = 0; c < M0; ++c) q1[c] = c < m0 ? S[c * 33 + i] : 0.0;
@@ -236,7 +275,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
     double nrm2 = 0.0;
 #pragma unroll
     for (int r = 0; r < 32; ++r) nrm2 = fma(mrow[r], mrow[r], nrm2);
-    const double nrm = sqrt(nrm2);
+    const double inrm = frsq(nrm2); // (the selection's scale: 1 / |M row i|)
     int dim;
     {
         double qq[M0];
@@ -249,13 +288,20 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         dim = n - rk; // independent bound normals the loop can hold (rank cap)
     }
     const bool eqb = lo == hi;
-    lds_barrier(); // every lane has its Q1 column: the region is the loop's now
+    cs_order(); // every lane has its Q1 column: the region is the loop's now
+    // GA and T are read (masked or against zero vector entries) past the live slots: finite from the start
+#pragma unroll
+    for (int j = 0; j < KM; ++j) S[L::GA + i * GS + j] = 0.0;
+#pragma unroll
+    for (int j = 0; j < (KM * (KM + 1) / 2 + 31) / 32; ++j)
+        if (j * 32 + i < KM * (KM + 1) / 2) S[L::TP + j * 32 + i] = 0.0;
     S[L::WV + i] = u0;
-    lds_barrier();
+    cs_order();
     double s = cs_rdot(mrow, S + L::WV); // s = M u0
     double u = u0, x = s;
     CsSlots g;
     bool onact = false;
+    WBQ_LAP(0);
     infeasible = false;
     bool dirty = false;
     // ------------------------------------------------ warm start: the last active set in one batch
@@ -272,7 +318,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
             rem &= rem ? rem - 1u : 0u;
             const double sj = (double)cs_bcast_i(wsg, j);
             double cpp;
-            const double c = cs_column<M0>(S, mrow, q1, i, j, cpp);
+            const double c = cs_column<M0>(S, mrow, q1, vcol, i, j, cpp);
             const double cg = __shfl(c, g.act, 32);
             const double v = (on && i < a2) ? g.sg * sj * cg : 0.0;
             double l, r;
@@ -294,6 +340,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 g.beta = sj > 0.0 ? loj : -hij;
             }
         }
+        WBQ_LAP(1);
         // multipliers of the batch optimum from u0: K lambda = beta_W - sg_W s_W
         const int kk = dep ? 0 : kw;
         const double xa = __shfl(s, g.act, 32);
@@ -303,8 +350,8 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         const bool bad = imax<32>((i < kk && !g.aeq && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
         const bool keep = kk > 0 && !bad;
         S[L::RV + i] = (keep && i < kk) ? g.sg * lw : 0.0;
-        lds_barrier();
-        const double dsw = cs_sdot(S + L::GA + i * GS, S + L::RV, keep ? kk : 0, kwmax < KM ? kwmax : KM);
+        cs_order();
+        const double dsw = cs_gdot(S + L::GA + i * GS, S + L::RV, kwmax < KM ? kwmax : KM);
         if (keep) {
             s += dsw;
             if (i < kk) g.lam = g.aeq ? lw : fmax(lw, 0.0);
@@ -313,6 +360,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
             iters += 1;
             dirty = true;
         }
+        WBQ_LAP(2);
     }
     // ------------------------------------------------ the loop
     const int maxit = a.max_iter;
@@ -342,7 +390,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 for (int a3 = cd; a3 + 1 < g.k; ++a3) S[L::GA + i * GS + a3] = S[L::GA + i * GS + a3 + 1];
                 --g.k;
             }
-            lds_barrier();
+            cs_order();
             const int amin = cs_wmin(dr ? cd : KM), amax = cs_wmax(dr ? g.k : 0);
             for (int a2 = amin; a2 < amax; ++a2) {
                 const bool on = dr && a2 >= cd && a2 < g.k;
@@ -357,7 +405,8 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 if (on && i == a2) S[L::TP + a2 * (a2 + 1) / 2 + a2] = id;
             }
             cdrop = -1;
-            lds_barrier();
+            cs_order();
+            WBQ_LAP(6);
         }
         bool rb = false;
         if (need_select) {
@@ -365,7 +414,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
             if (go && row && !onact) {
                 const double tol = 1e-10 * fmax(1.0, fmax(fabs(s), fmax(fabs(lo), fabs(hi))));
                 const double viol = fmax(lo - s, s - hi);
-                if (viol > tol) v = viol / nrm;
+                if (viol > tol) v = viol * inrm;
             }
             int pi = i;
             iargmax<32>(v, pi);
@@ -383,6 +432,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 have_col = false;
             }
         }
+        WBQ_LAP(3);
         if (__any(rb)) {
             // u and x from the multipliers, refinement on the active set, then every bound re-checked
             cs_rebuild<M0>(S, mrow, q1, i, rb, g, u0, u, x);
@@ -414,18 +464,22 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                     go = false;
                 }
             }
+            WBQ_LAP(7);
+            WBQ_LAP_ADD(1, 1);
             continue;
         }
         if (!__any(go)) break;
         if (__any(go && !have_col)) { // (a drop keeps stepping on p: its column is kept)
             double cppn;
-            const double cn = cs_column<M0>(S, mrow, q1, i, p, cppn);
+            const double cn = cs_column<M0>(S, mrow, q1, vcol, i, p, cppn);
             if (!have_col) {
                 c = cn;
                 cpp = cppn;
                 have_col = true;
             }
         }
+        WBQ_LAP(4);
+        WBQ_LAP_ADD(0, 1);
         // ---- the step for bound p
         const int k = g.k, kmx = cs_wmax(go ? k : 0);
         const double cg = __shfl(c, g.act, 32); // Gamma[act_a][p] on slot lane a
@@ -434,16 +488,16 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         cs_tsolve(S, i, v, go ? k : 0, kmx, l, r);
         const double d2 = cpp - isum<32>(l * l);
         S[L::RV + i] = (go && i < k) ? g.sg * r : 0.0;
-        lds_barrier();
-        const double ds = sgp * c - cs_sdot(S + L::GA + i * GS, S + L::RV, go ? k : 0, kmx);
+        cs_order();
+        const double ds = sgp * c - cs_gdot(S + L::GA + i * GS, S + L::RV, kmx);
         const double zz = sgp * cs_bcast(ds, p);
         const double slack = sgp * (cs_bcast(s, p) - bnd); // < 0: violated
         const double rmax = imax<32>(i < k ? fabs(r) : 0.0);
-        double cand = (i < k && !g.aeq && r > 1e-13 * rmax) ? g.lam / r : kInf;
+        double cand = (i < k && !g.aeq && r > 1e-13 * rmax) ? g.lam * frcp(r) : kInf;
         int ci = i;
         iargmin<32>(cand, ci);
         const double t1 = cand;
-        const double t2 = (k < dim && d2 > kCsDep * cpp && zz > 0.0) ? -slack / zz : kInf;
+        const double t2 = (k < dim && d2 > kCsDep * cpp && zz > 0.0) ? -slack * frcp(zz) : kInf;
         if (go) {
             if (t1 >= kInf && t2 >= kInf) {
                 // no step: the bounds cannot all be met -- unless the incremental activities drifted; then
@@ -490,19 +544,21 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 }
             }
         }
-        lds_barrier();
+        WBQ_LAP(5);
     }
     if (record) { // the final active set, by joint, for the next solve of this instance
-        lds_barrier();
+        cs_order();
         S[L::VV + i] = 0.0;
-        lds_barrier();
+        cs_order();
         if (i < g.k && !g.aeq) S[L::VV + g.act] = g.sg;
-        lds_barrier();
+        cs_order();
         const double sgn = S[L::VV + i];
         const bool ok = status == 0 && !infeasible;
         if (row && a.ws_rows) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
-        lds_barrier();
+        cs_order();
     }
+    WBQ_LAP(3);
+    if constexpr (LAPB > 0) WBQ_LAP_FLUSH(LAPB, LAPC);
     u_out = u;
     return x;
 }

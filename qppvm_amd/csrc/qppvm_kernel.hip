@@ -1589,7 +1589,17 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
             WBQ_STAMP(18); // (diagnostic build: the inline dual active set starts)
             double x2, u2;
             if constexpr (NP == 32 && WBQ_GI_CS != 0) {
-                x2 = cs_solve<M0>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2);
+                // this lane's column of V = Q1 M = L^-1 G M: forward substitution of Y's row (Y = M G^T)
+                double vcol[M0];
+#pragma unroll
+                for (int c = 0; c < M0; ++c) {
+                    double v = (c < m0) ? Y[c] : 0.0;
+#pragma unroll
+                    for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], vcol[k], v);
+                    vcol[c] = v * il[c];
+                }
+                x2 = cs_solve<M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2,
+                                          vcol);
             } else {
                 x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true);
                 u2 = S[LA.U + i];

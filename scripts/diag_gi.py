@@ -18,7 +18,11 @@ import bench  # noqa: E402
 from qppvm_amd import wbq  # noqa: E402
 
 K = 64
-LAPS = ["setup", "warm_batch", "warm_step", "select", "project_out", "step_add_drop", "rebuild", "record"]
+# the u-space loop (gi_solve, rounds 1-5; WBQ_GI_CS=0 builds) or the constraint-space loop (cs_gi.h, round 6:
+# counts 13 = passes, 14 = x rebuilds)
+LAPS = (["setup", "warm_batch", "warm_step", "select", "project_out", "step_add_drop", "rebuild", "record"]
+        if os.environ.get("WBQ_DIAG_LOOP", "cs") == "gs" else
+        ["setup", "warm_append", "warm_lambda", "select", "column", "step", "drop", "rebuild_refine"])
 
 
 def stamps(s, nb):
@@ -49,6 +53,10 @@ def summarise(full, rollout=False):
         rb = rebuilds[g] > 0
         if rb.any():
             out["gi_cycles_per_rebuild_projection_p50"] = float(np.median(laps[g, 6][rb] / rebuilds[g][rb]))
+    gi_tot = laps.sum(1)
+    order = np.argsort(-gi_tot)[:6]
+    out["most_gi_cycles"] = [{"block": int(b), "gi_cycles": int(gi_tot[b]), "passes": int(passes[b]),
+                              "rebuilds": int(rebuilds[b]), "laps": [int(x) for x in laps[b]]} for b in order]
     rep = full[:, 7] > 0
     out["repair_blocks"] = int(rep.sum())
     if rep.any():
