@@ -250,13 +250,17 @@ constexpr double kCsDep = 1e-14;   // a row whose Schur complement is below kCsD
 // QA) on entry; vcol = this lane's column of V = Q1 M (the fast path has it from Y = M G^T: V^T = Y L^-T). Returns this lane's x = M u (exact, rebuilt); u_out = u. status 1: step cap; infeasible: no
 // step exists (level 0 not attainable at b0 inside the bounds) or the hand-off described above. wsg: the
 // warm side of this lane's bound (+1 lower, -1 upper, 0 none); record: the final active set to ws_rows.
+// bail: the hand-off described at the head of this file (more than KM active bounds, an active bound the rebuilt
+// x misses, the rebuild-round cap); with VIN false the instance's Q1 rows are back in LDS then, so the u-space
+// loop can take it.
 // (LAPB / LAPC: stamp slots of the diagnostic build's lap counters, as gi_solve: 8 phases from LAPB -- setup,
 // warm appends, warm multipliers, select, column, step, drop, rebuild -- and 2 counts from LAPC: passes, rebuilds)
-template <int M0, int LAPB = 0, int LAPC = 0>
+// VIN: vcol is given (the fast path); else it is formed here from Q1's rows in LDS (the repair)
+template <int M0, int LAPB = 0, int LAPC = 0, bool VIN = true>
 __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u0, int &status, int &iters,
                                            bool &infeasible, int wsg, bool record, double &u_out,
-                                           const double (&vcol)[M0])
+                                           const double (&vin)[M0], bool &bail)
 {
     using L = CsLayout;
     constexpr int KM = L::KM, GS = L::GS;
@@ -276,6 +280,21 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
     for (int r = 0; r < 32; ++r) nrm2 = fma(mrow[r], mrow[r], nrm2);
     const double inrm = frsq(nrm2); // (the selection's scale: 1 / |M row i|)
+    double vcol[M0];
+    if constexpr (VIN) {
+#pragma unroll
+        for (int c = 0; c < M0; ++c) vcol[c] = vin[c];
+    } else { // V[c][i] = Q1 row c . M column i
+#pragma unroll
+        for (int c = 0; c < M0; ++c) {
+            double v = 0.0;
+            if (c < m0)
+#pragma unroll
+                for (int r = 0; r < 32; ++r) v = fma(S[c * 33 + r], mrow[r], v);
+            vcol[c] = v;
+        }
+    }
+    bail = false;
     int dim;
     {
         double qq[M0];
@@ -452,7 +471,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 const double xa = __shfl(x, g.act, 32);
                 const double miss = (rb && i < g.k) ? fabs(g.beta - g.sg * xa) / (1.0 + fabs(xa)) : 0.0;
                 if (rb && imax<32>(miss) > 1e-8) {
-                    infeasible = true;
+                    bail = true;
                     go = false;
                 }
             }
@@ -460,7 +479,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 s = x;
                 dirty = false;
                 if (++rounds > kCsRounds && go) {
-                    infeasible = true;
+                    bail = true;
                     go = false;
                 }
             }
@@ -510,7 +529,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                     go = false;
                 }
             } else if (t2 <= t1 && k >= KM) {
-                infeasible = true; // slot storage: hand off
+                bail = true; // slot storage: hand off
                 go = false;
             } else {
                 dirty = true;
@@ -559,6 +578,13 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
     }
     WBQ_LAP(3);
     if constexpr (LAPB > 0) WBQ_LAP_FLUSH(LAPB, LAPC);
+    if (!VIN && __any(bail)) { // (the repair) Q1's rows back where the u-space loop reads them
+        cs_order();
+#pragma unroll
+        for (int c = 0; c < M0; ++c)
+            if (bail && c < m0) S[c * 33 + i] = q1[c];
+        cs_order();
+    }
     u_out = u;
     return x;
 }

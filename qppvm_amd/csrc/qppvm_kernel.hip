@@ -695,9 +695,34 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
             return;
         }
     }
-    if (__any(rep && !uniq))
-        x_i = gi_solve<NP, M0, 48, 56>(a, S, b, i, row, rep && status == 0 && !uniq, ro.lo, ro.hi, ro.u, status, iters,
-                               infeasible, wsr, true);
+    if (__any(rep && !uniq)) {
+        const bool g1 = rep && status == 0 && !uniq;
+        if constexpr (NP == 32 && WBQ_GI_CS != 0) {
+            // the pinned level 1 by the constraint-space loop (cs_gi.h); a hand-off there takes the u-space loop
+            bool bail;
+            double uo;
+            const double vnone[M0] = {};
+            x_i = cs_solve<M0, 48, 56, false>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr,
+                                              true, uo, vnone, bail);
+            if (__any(bail)) {
+                int st3 = 0, it3 = 0;
+                bool inf3 = false;
+                const double x3 = gi_solve<NP, M0>(a, S, b, i, row && bail, bail, ro.lo, ro.hi, ro.u, st3, it3, inf3, wsr,
+                                                   true);
+                if (bail) {
+                    x_i = x3;
+                    status = st3;
+                    iters += it3;
+                    infeasible = inf3;
+                }
+            }
+            __syncthreads();
+            if (!bail) S[L.U + i] = uo; // (rollout_step below reads u there; gi_solve wrote every lane's)
+            __syncthreads();
+        } else {
+            x_i = gi_solve<NP, M0, 48, 56>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr, true);
+        }
+    }
     if (uniq) x_i = ro.x;
     if (a.integrate && __any(rep && uniq)) { // rollouts integrate qdd = u = M^-1 x*
         const bool r2 = row && uniq;
@@ -1598,8 +1623,10 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
                     for (int k = 0; k < c; ++k) v = fma(-Lm[c * (c + 1) / 2 + k], vcol[k], v);
                     vcol[c] = v * il[c];
                 }
+                bool bail;
                 x2 = cs_solve<M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2,
-                                          vcol);
+                                          vcol, bail);
+                inf |= bail; // (the level-0 repair takes a hand-off: its u-space loop settles it)
             } else {
                 x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true);
                 u2 = S[LA.U + i];
