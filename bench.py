@@ -181,12 +181,38 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
         pool = churn_pool(form, prob, n, B, world, rank)
         keys = list(inp.keys())
         dev = f"cuda:{device}"
-        live = {k: torch.from_numpy(np.ascontiguousarray(inp[k])).to(dev) for k in keys}
-        alt = [{k: live[k].clone() for k in keys},
-               {k: torch.from_numpy(np.ascontiguousarray(pool[k])).to(dev) for k in keys}]
+        # every field of a dtype lives in one flat device buffer (each field a contiguous view, the layout the
+        # solver adopts), so that a refresh is one gather + one scatter over precomputed element indices per
+        # dtype -- the same rows of every field -- instead of one copy dispatch per field (eight ~5 us copy
+        # kernels took ~35 us of a ~140 us step: profiles/r06_v7_ab_nograph_c2.log; a captured graph of the
+        # copies did not shorten it on ROCm 7.2)
+        groups = {}
+        for k in keys:
+            groups.setdefault(np.asarray(inp[k]).dtype.str, []).append(k)
+        sl = (B + 4) // 5
+        flat, live, alt0, alt1, idx = {}, {}, {}, {}, {}
+        for dt, ks in groups.items():
+            sizes = [int(np.prod(np.asarray(inp[k]).shape)) for k in ks]
+            offs = np.concatenate([[0], np.cumsum(sizes)])
+            tdt = torch.from_numpy(np.zeros(1, dtype=np.dtype(dt))).dtype
+            f_live = torch.empty(int(offs[-1]), dtype=tdt, device=dev)
+            f_alt0, f_alt1 = torch.empty_like(f_live), torch.empty_like(f_live)
+            for k, o, sz in zip(ks, offs[:-1], sizes):
+                shp = np.asarray(inp[k]).shape
+                live[k] = f_live[o:o + sz].view(shp)
+                live[k].copy_(torch.from_numpy(np.ascontiguousarray(inp[k])).to(dev))
+                f_alt0[o:o + sz].copy_(live[k].reshape(-1))
+                f_alt1[o:o + sz].view(shp).copy_(torch.from_numpy(np.ascontiguousarray(pool[k])).to(dev))
+            # element indices of row slice q of every field of this dtype
+            idx[dt] = []
+            for q in range(5):
+                lo, hi = q * sl, min(B, (q + 1) * sl)
+                per = [np.arange(o + lo * (sz // B), o + hi * (sz // B)) for o, sz in zip(offs[:-1], sizes)]
+                idx[dt].append(torch.from_numpy(np.concatenate(per)).to(dev))
+            flat[dt] = (f_live, (f_alt0, f_alt1))
         solver.set_stream(torch.cuda.current_stream(device).cuda_stream)
         solver.set_device_inputs({k: live[k].data_ptr() for k in keys}, B)
-        churn = dict(live=live, alt=alt, calls=0, slice=(B + 4) // 5)
+        churn = dict(flat=flat, idx=idx, calls=0)
         torch.cuda.synchronize()
 
     rbd = None
@@ -207,13 +233,10 @@ def run(form, config, n, B, steps, warmup, world, rank, device, allgather=False,
             return
         if churn is not None:
             c = churn["calls"]
-            lo = (c % 5) * churn["slice"]
-            src = churn["alt"][1 - (c // 5) % 2]  # pool states, then the originals, ...
-            # every field's rows in one multi-tensor copy launch (the same bytes as one copy per field, whose ten
-            # launches took ~30 us of a ~150 us step on MI355X: profiles/r06_v4_ab_*_c2.log step vs kernel)
-            sl = churn["slice"]
-            keys = list(churn["live"].keys())
-            torch._foreach_copy_([churn["live"][k][lo:lo + sl] for k in keys], [src[k][lo:lo + sl] for k in keys])
+            for dt, (f_live, alts) in churn["flat"].items():
+                ix = churn["idx"][dt][c % 5]
+                src = alts[1 - (c // 5) % 2]  # pool states, then the originals, ...
+                f_live.index_copy_(0, ix, src.index_select(0, ix))
             churn["calls"] = c + 1
         if config == 4:
             solver.set_state(q0.data_ptr(), qd0.data_ptr(), device=True)

@@ -255,12 +255,13 @@ constexpr double kCsDep = 1e-14;   // a row whose Schur complement is below kCsD
 // loop can take it.
 // (LAPB / LAPC: stamp slots of the diagnostic build's lap counters, as gi_solve: 8 phases from LAPB -- setup,
 // warm appends, warm multipliers, select, column, step, drop, rebuild -- and 2 counts from LAPC: passes, rebuilds)
-// VIN: vcol is given (the fast path); else it is formed here from Q1's rows in LDS (the repair)
+// VIN: vcol and x0 = M u0 are given (the fast path); else they are formed here (vcol from Q1's rows in LDS: the
+// repair)
 template <int M0, int LAPB = 0, int LAPC = 0, bool VIN = true>
 __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u0, int &status, int &iters,
                                            bool &infeasible, int wsg, bool record, double &u_out,
-                                           const double (&vin)[M0], bool &bail)
+                                           const double (&vin)[M0], bool &bail, double x0 = 0.0)
 {
     using L = CsLayout;
     constexpr int KM = L::KM, GS = L::GS;
@@ -314,9 +315,14 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
     for (int j = 0; j < (KM * (KM + 1) / 2 + 31) / 32; ++j)
         if (j * 32 + i < KM * (KM + 1) / 2) S[L::TP + j * 32 + i] = 0.0;
-    S[L::WV + i] = u0;
-    cs_order();
-    double s = cs_rdot(mrow, S + L::WV); // s = M u0
+    double s;
+    if constexpr (VIN) {
+        s = x0; // the fast path's x = M u0 (the activities its bound check saw)
+    } else {
+        S[L::WV + i] = u0;
+        cs_order();
+        s = cs_rdot(mrow, S + L::WV); // s = M u0
+    }
     double u = u0, x = s;
     CsSlots g;
     bool onact = false;

@@ -1625,7 +1625,7 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
                 }
                 bool bail;
                 x2 = cs_solve<M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2,
-                                          vcol, bail);
+                                          vcol, bail, x_i);
                 inf |= bail; // (the level-0 repair takes a hand-off: its u-space loop settles it)
             } else {
                 x2 = gi_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true);
