@@ -26,8 +26,11 @@ if [ "$STEPS" = "a" ]; then
   cd /tmp
   for cfg in 1 2 4; do # kernel statistics of the bench configurations (the bench lines' event times beside them)
     st=200; [ $cfg = 4 ] && st=10
+    # (one launch shape per summary: no contact-form variant, and config 4 without the one-step launches of the
+    # repair-share pass)
+    ex="--no-variant"; [ $cfg = 4 ] && ex="--no-variant --no-repair-share"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_cfg$cfg" -o run --output-format csv -- \
-        python3 "$ROOT/bench.py" --config $cfg --steps $st --warmup 5 --no-cpu --no-pmc > "$ROOT/gpurun_out/prof_cfg$cfg.log" 2>&1
+        python3 "$ROOT/bench.py" --config $cfg --steps $st --warmup 5 --no-cpu --no-pmc $ex > "$ROOT/gpurun_out/prof_cfg$cfg.log" 2>&1
     rc=$?; echo "prof cfg$cfg rc=$rc"
     [ $rc -ne 0 ] && exit 1
   done
