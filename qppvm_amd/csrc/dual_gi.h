@@ -25,6 +25,24 @@
 
 namespace wbq {
 
+// LDS ordering inside the loop (round 6). Every kernel that runs this loop is one wave per workgroup, and the LDS
+// unit executes one wave's DS instructions in issue order: a write by one lane is seen by a later read of another
+// lane of the same wave without a workgroup barrier, so only the compiler must keep the order. __syncthreads()
+// is a workgroup fence on every address space: it waits for all of the wave's outstanding memory accesses
+// (s_waitcnt vmcnt(0) lgkmcnt(0)) at each of the loop's ~30 uses. WBQ_GI_WAVE_LDS = 0: __syncthreads() (A/B).
+#ifndef WBQ_GI_WAVE_LDS
+#define WBQ_GI_WAVE_LDS 1
+#endif
+__device__ __forceinline__ void gi_sync()
+{
+#if WBQ_GI_WAVE_LDS
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    __syncthreads();
+#endif
+}
+
 // Per-lane vector of active-slot values (T rows, T columns, Gamma columns of the active
 // set): in registers (KM static; dynamic writes by select) or one LDS row per lane, whose
 // dots load in chunks of 8 independent reads. Either way the loads of a dot issue back to
@@ -272,7 +290,7 @@ __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k,
         const double sc = __shfl(g.sgn, c);
         if (own) S[tb + i * ts + c] = c <= i ? g.sgn * sc * pb.gamma(g.act, ac) : 0.0;
     }
-    __syncthreads();
+    gi_sync();
     const double *ri = S + tb + (own ? i : 0) * ts;
 #pragma unroll 1
     for (int c = 0; c < k; ++c) {
@@ -292,7 +310,7 @@ __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k,
         const double d = fmax(bcast(s, c), 1e-30 * gcc); // a non-positive pivot: the miss check drops it
         const double il = frsq(d);
         if (own && i >= c) S[tb + i * ts + c] = i == c ? d * il : s * il;
-        __syncthreads();
+        gi_sync();
     }
 #pragma unroll 1
     for (int c = k - 1; c >= 0; --c) {
@@ -300,9 +318,9 @@ __device__ void refactor_T(const P &pb, double *S, int tb, int ts, int i, int k,
         double acc = 0.0;
         if (own && i > c)
             for (int q = c + 1; q <= i; ++q) acc = fma(ri[q], S[tb + q * ts + c], acc);
-        __syncthreads();
+        gi_sync();
         if (own && i >= c) S[tb + i * ts + c] = i == c ? 1.0 / lcc : -acc / lcc;
-        __syncthreads();
+        gi_sync();
     }
 }
 
@@ -332,10 +350,10 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
         const double gpp = pb.gamma(cp, cp);
         S[V.VV + i] = i < k ? g.sgn * sgp * pb.gamma(g.act, cp) : 0.0;
         S[V.AC + i] = (double)g.act;
-        __syncthreads();
+        gi_sync();
         const double l = i < k ? Trow.dot(S + V.VV, k) : 0.0;
         S[V.LV + i] = l;
-        __syncthreads();
+        gi_sync();
         const double r = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
         const double d2 = gpp - isum<64>(l * l);
         if (!(d2 > P::kDep * gpp)) { // dependent on the set: no warm start
@@ -347,7 +365,7 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
         Tcol.put_dyn(k, i <= k, tk);
         GA.put_dyn(k, kind != 0, kind != 0 ? pb.gamma(i, cp) : 0.0);
         S[V.WV + i] = tk;
-        __syncthreads();
+        gi_sync();
         Trow.load_if(i == k, S + V.WV, k + 1);
         if (i == k) {
             g.act = cp;
@@ -356,17 +374,17 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
             g.lam = 0.0;
         }
         ++k;
-        __syncthreads();
+        gi_sync();
     }
     if (ok) { // dlambda = T^T T (b_A - s_A); rows already in have zero residual
         const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act), s_a = __shfl(s_i, g.act);
         const double res = (i >= k0 && i < k) ? g.sgn * ((g.sgn > 0.0 ? lo_a : hi_a) - s_a) : 0.0;
         S[V.VV + i] = res;
         S[V.AC + i] = (double)g.act;
-        __syncthreads();
+        gi_sync();
         const double y = i < k ? Trow.dot(S + V.VV, k) : 0.0;
         S[V.LV + i] = y;
-        __syncthreads();
+        gi_sync();
         const double dl = i < k ? Tcol.dot(S + V.LV, k) : 0.0;
         const double lam = g.lam + dl;
         const double lmx = imax<64>(i < k ? fabs(lam) : 0.0);
@@ -374,11 +392,11 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
         if (ok) {
             if (i < k) g.lam = g.aeq ? lam : fmax(lam, 0.0);
             S[V.RV + i] = i < k ? g.sgn * dl : 0.0;
-            __syncthreads();
+            gi_sync();
             if (kind != 0) s_i += GA.dot(S + V.RV, k);
             if (isw) g.onact = true;
             g.k = k;
-            __syncthreads();
+            gi_sync();
             return true;
         }
     }
@@ -395,7 +413,7 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
         g.aeq = d0.aeq;
     }
     S[V.AC + i] = (double)g.act;
-    __syncthreads();
+    gi_sync();
     return false;
 }
 
@@ -404,11 +422,11 @@ __device__ bool warm_extend(const P &pb, double *S, const GiVecs &V, int i, Trow
 __device__ __forceinline__ int warm_record(double *S, const GiVecs &V, int i, const GiState &g)
 {
     S[V.WV + i] = 0.0;
-    __syncthreads();
+    gi_sync();
     if (i < g.k && !g.aeq) S[V.WV + g.act] = g.sgn;
-    __syncthreads();
+    gi_sync();
     const double v = S[V.WV + i];
-    __syncthreads();
+    gi_sync();
     return v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
 }
 
@@ -447,24 +465,24 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             --g.k;
             Trow.zero_if(i >= drop);
             Tcol.zero_from(drop);
-            __syncthreads();
+            gi_sync();
             for (int a2 = drop; a2 < g.k; ++a2) {
                 const int cq = __shfl(g.act, a2);
                 const double sq = __shfl(g.sgn, a2);
                 S[V.VV + i] = i < a2 ? g.sgn * sq * pb.gamma(g.act, cq) : 0.0;
-                __syncthreads();
+                gi_sync();
                 const double l2 = i < a2 ? Trow.dot(S + V.VV, a2) : 0.0;
                 S[V.LV + i] = l2;
-                __syncthreads();
+                gi_sync();
                 const double r2 = i < a2 ? Tcol.dot(S + V.LV, a2) : 0.0;
                 const double e2 = pb.gamma(cq, cq) - isum<64>(l2 * l2);
                 const double id2 = e2 > 0.0 ? frsq(e2) : 0.0;
                 const double tk2 = i < a2 ? -r2 * id2 : (i == a2 ? id2 : 0.0);
                 Tcol.put_dyn(a2, i <= a2, tk2);
                 S[V.WV + i] = tk2;
-                __syncthreads();
+                gi_sync();
                 Trow.load_if(i == a2, S + V.WV, a2 + 1);
-                __syncthreads();
+                gi_sync();
             }
             drop = -1;
         }
@@ -502,7 +520,7 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                 const double lo_a = __shfl(lo, g.act), hi_a = __shfl(hi, g.act); // all lanes active
                 S[V.RV + i] = i < g.k ? g.sgn * g.lam : 0.0;
                 S[V.AC + i] = (double)g.act;
-                __syncthreads();
+                gi_sync();
 #pragma unroll 1
                 for (int pass = 0; pass < kGiPasses; ++pass) {
                     if (pass > 0) {
@@ -519,17 +537,17 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
                         // a nearly dependent active set gains ~eps cond(Gamma_AA) per pass
                         if (pass > 2 && imax<64>(i < g.k ? fabs(res) / (1.0 + fabs(a_act)) : 0.0) <= 1e-13) break;
                         S[V.VV + i] = res;
-                        __syncthreads();
+                        gi_sync();
                         const double y = Trow.dot(S + V.VV, g.k);
                         S[V.LV + i] = i < g.k ? y : 0.0;
-                        __syncthreads();
+                        gi_sync();
                         const double dl = i < g.k ? Tcol.dot(S + V.LV, g.k) : 0.0;
                         g.lam += dl;
                         S[V.RV + i] = i < g.k ? g.sgn * dl : 0.0;
-                        __syncthreads();
+                        gi_sync();
                     }
                     pb.rebuild(pass, g.k);
-                    __syncthreads();
+                    gi_sync();
                 }
                 if (kind != 0) s_i = pb.activity(i);
                 // the active rows must hold at the rebuilt x; if one does not, T (the factor
@@ -575,14 +593,14 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
         const double gpp = pb.gamma(cp, cp);
         S[V.VV + i] = i < g.k ? g.sgn * sgp * pb.gamma(g.act, cp) : 0.0;
         S[V.AC + i] = (double)g.act;
-        __syncthreads();
+        gi_sync();
         const double l = i < g.k ? Trow.dot(S + V.VV, g.k) : 0.0;
         S[V.LV + i] = l;
-        __syncthreads();
+        gi_sync();
         const double r = i < g.k ? Tcol.dot(S + V.LV, g.k) : 0.0;
         const double d2 = gpp - isum<64>(l * l);
         S[V.RV + i] = i < g.k ? g.sgn * r : 0.0;
-        __syncthreads();
+        gi_sync();
         const double gjp = (kind != 0) ? pb.gamma(i, cp) : 0.0;
         const double ds = (kind != 0) ? sgp * gjp - GA.dot(S + V.RV, g.k) : 0.0;
         const double zz = sgp * __shfl(ds, cp);
@@ -625,7 +643,7 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             Tcol.put_dyn(g.k, i <= g.k, tk);
             GA.put_dyn(g.k, kind != 0, gjp);
             S[V.WV + i] = tk;
-            __syncthreads();
+            gi_sync();
             Trow.load_if(i == g.k, S + V.WV, g.k + 1);
             if (i == g.k) {
                 g.act = cp;
@@ -636,7 +654,7 @@ __device__ __forceinline__ void dual_gi(const P &pb, double *S, const GiVecs &V,
             if (i == cp) g.onact = true;
             ++g.k;
             need_select = true;
-            __syncthreads();
+            gi_sync();
         } else { // drop slot blk (its multiplier reached zero), keep stepping on cp
             drop = blk;
             need_select = false;
