@@ -84,6 +84,23 @@
 namespace wbq {
 namespace {
 
+// LDS ordering inside the u-space loop (gi_solve, project_out; round 6): every kernel that runs it is one wave per
+// workgroup and the LDS unit executes one wave's DS instructions in issue order, so a compiler fence orders a
+// lane's write before another lane's later read; __syncthreads() also waited for every outstanding memory access
+// (s_waitcnt vmcnt(0) lgkmcnt(0)) at each of the loop's barriers. WBQ_GS_WAVE_LDS = 0: __syncthreads() (A/B).
+#ifndef WBQ_GS_WAVE_LDS
+#define WBQ_GS_WAVE_LDS 1
+#endif
+__device__ __forceinline__ void gs_sync()
+{
+#if WBQ_GS_WAVE_LDS
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    __syncthreads();
+#endif
+}
+
 // Per-instance LDS layouts in doubles (T = ntasks and m0 are launch constants). Rows of
 // NP-wide matrices use stride NP+1 so that lane-per-row reads are bank-conflict free.
 template <int NP>
@@ -174,19 +191,19 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
     // spilled the n <= 32 fast kernel that inlines this loop, 0 -> ~300 B of scratch even at 4-element chunks)
     const double d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
     S[L.D1 + i] = d1;
-    __syncthreads();
+    gs_sync();
     double z = npj - dot4s<NP>(S + L.QA + i, RS, S + L.D1);
     zz = isum<NP>(z * z);
     if (__any(act && !(zz > 0.5 * nn2))) {
         S[L.BC + i] = z;
-        __syncthreads();
+        gs_sync();
         const double d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
         S[L.D1B + i] = d1b;
-        __syncthreads();
+        gs_sync();
         z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
         S[L.D1 + i] = d1 + d1b;
         zz = isum<NP>(z * z);
-        __syncthreads();
+        gs_sync();
     }
     return z;
 }
@@ -258,7 +275,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     const int maxit = a.max_iter;
     const bool eqb = lo == hi;
     infeasible = false;
-    __syncthreads();
+    gs_sync();
     WBQ_LAP(0);
     if (__any(go && row && wsg != 0)) {
         // ------------------------------------------------ warm start: the last active set in one batch
@@ -271,7 +288,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         int kwmax = kw;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) kwmax = max(kwmax, __shfl_xor(kwmax, m, 64));
-        __syncthreads();
+        gs_sync();
         const int myp = i < kw ? (int)S[L.BC + i] : 0; // this slot lane's joint
         bool dep = false;
         for (int a2 = 0; a2 < kwmax; ++a2) {
@@ -280,7 +297,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             const int sa = __shfl(wsg, pa, NP);
             const double nj = on ? sa * Mr.get(pa) : 0.0;
             S[L.NV + i] = nj;
-            __syncthreads();
+            gs_sync();
             const double npn = __shfl(nrm, pa, NP);
             double zzr;
             const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr);
@@ -294,7 +311,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 if (i == a2) Tr.set(a2, iz);
                 ++q;
             }
-            __syncthreads();
+            gs_sync();
         }
         WBQ_LAP(1);
         // residuals r_a = beta_a - n_a . u on the slot lanes, w = T^T r (lane j: w_j), lambda = T w
@@ -311,7 +328,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             }
         }
         S[L.BC + i] = i < kw ? w_own : 0.0;
-        __syncthreads();
+        gs_sync();
         const double lw = i < kw ? Tr.dot(S + L.BC, NP) : 0.0;
         const bool peqw = __shfl(eqb ? 1 : 0, myp, NP) != 0;
         const double lmx = imax<NP>(fabs(lw));
@@ -334,9 +351,9 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             Tr.zero();
             q = m0;
         }
-        __syncthreads();
+        gs_sync();
         S[L.U + i] = u_i;
-        __syncthreads();
+        gs_sync();
         WBQ_LAP(2);
     }
     while (true) {
@@ -363,7 +380,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         const bool peq = __shfl(eqb ? 1 : 0, p, NP) != 0;
         const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
         S[L.NV + i] = npj;
-        __syncthreads();
+        gs_sync();
         WBQ_LAP(3);
         double zz;
         const double z = project_out<NP>(S, L, npj, q, i, npn * npn, go, zz);
@@ -435,7 +452,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             }
         }
         S[L.U + i] = u_i;
-        __syncthreads();
+        gs_sync();
         WBQ_LAP(5);
         if (__any(rebuild)) {
           if constexpr (kGivens) {
@@ -452,7 +469,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
                 for (int j = 0; j < NP; ++j) S[L.BC + j] = Tr.at(j); // row c of T, every lane reads it
             }
-            __syncthreads();
+            gs_sync();
             double xr = rebuild ? S[L.BC + cdrop] : 0.0; // the chase's running entry
 #pragma unroll
             for (int j = 0; j + 1 < NP; ++j) {
@@ -480,7 +497,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 double nrow[NP];
 #pragma unroll
                 for (int j = 0; j < NP; ++j) nrow[j] = __shfl(Tr.at(j), nxt, NP);
-                __syncthreads(); // (T rows in LDS: every read of row i + 1 before its owner writes it)
+                gs_sync(); // (T rows in LDS: every read of row i + 1 before its owner writes it)
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
                     double v = (rebuild && i >= cdrop) ? nrow[j] : Tr.at(j);
@@ -489,7 +506,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 }
             }
             if (rebuild) q = m0 + k;
-            __syncthreads();
+            gs_sync();
             WBQ_LAP_ADD(1, 1);
           } else {
             // Re-factor the inequality directions from the dropped position on: Q1T rows
@@ -511,7 +528,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 const int pa = __shfl(act_p, a2, NP), sa = __shfl(act_s, a2, NP);
                 const double nj = on ? sa * Mr.get(pa) : 0.0;
                 S[L.NV + i] = nj;
-                __syncthreads();
+                gs_sync();
                 const double npa = __shfl(nrm, pa, NP);
                 double zzr;
                 const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npa * npa, on, zzr);
@@ -524,7 +541,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                     if (i == a2) Tr.set(a2, iz);
                     ++q;
                 }
-                __syncthreads();
+                gs_sync();
                 WBQ_LAP_ADD(1, 1);
             }
           }
@@ -534,13 +551,13 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     WBQ_LAP(3); // (the last pass: select only)
     if (record) { // the final active set, by joint, for the next solve of this instance
         S[L.NV + i] = 0.0;
-        __syncthreads();
+        gs_sync();
         if (i < k && !act_e) S[L.NV + act_p] = (double)act_s;
-        __syncthreads();
+        gs_sync();
         const double sgn = S[L.NV + i];
         const bool ok = status == 0 && !infeasible;
         if (go_rec(row, b, a)) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
-        __syncthreads();
+        gs_sync();
     }
     const double xf = Mr.dot(S + L.U, NP);
     WBQ_LAP(7);
