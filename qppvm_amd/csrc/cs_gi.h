@@ -33,8 +33,10 @@ namespace wbq {
 
 // Per-instance LDS (doubles), inside ActiveLayout<32>'s 1,248 (the caller's Q1 rows at the start of the
 // region are read into registers first; GA then overlays them)
-struct CsLayout {
-    static constexpr int NP = 32, KM = 24, GS = KM + 1; // slots; GA row stride (odd: lane rows conflict-free)
+template <int NP_>
+struct CsLayoutT {
+    static constexpr int NP = NP_;
+    static constexpr int KM = NP == 32 ? 24 : 40, GS = KM + 1; // slots; GA row stride (odd: lane rows conflict-free)
     static constexpr int GA = 0;                        // [NP][GS] Gamma[i][act_a]
     static constexpr int TP = GA + NP * GS;             // T = L^-1, packed lower rows, KM (KM + 1) / 2
     static constexpr int WV = TP + KM * (KM + 1) / 2;   // w = P m_p, then u (broadcast vectors)
@@ -43,8 +45,11 @@ struct CsLayout {
     static constexpr int RV = LV + NP;                  // sg r
     static constexpr int SIZE = RV + NP;
 };
-static_assert(CsLayout::SIZE <= 32 * 33 + 6 * 32, "CsLayout fits ActiveLayout<32>");
-static_assert(CsLayout::WV % 2 == 0 && CsLayout::TP % 2 == 0, "16-byte aligned vectors");
+using CsLayout = CsLayoutT<32>;
+static_assert(CsLayoutT<32>::SIZE <= 32 * 33 + 6 * 32, "CsLayout fits ActiveLayout<32>");
+static_assert(CsLayoutT<64>::SIZE <= 64 * 65, "CsLayout<64> fits the QA region of ActiveLayout<64>");
+static_assert(CsLayoutT<32>::WV % 2 == 0 && CsLayoutT<32>::TP % 2 == 0, "16-byte aligned vectors");
+static_assert(CsLayoutT<64>::WV % 2 == 0 && CsLayoutT<64>::TP % 2 == 0, "16-byte aligned vectors");
 
 // LDS ordering inside the loop. The fast kernel's workgroup is one wave, and the LDS unit executes one wave's
 // DS instructions in issue order, so a write by one lane is seen by a later read of another lane of the same
@@ -65,47 +70,72 @@ __device__ __forceinline__ void cs_order()
 }
 
 // ---------------------------------------------------------------- NP = 32 lane helpers
-// value of v at lane idx of this lane's instance (idx instance-uniform): two v_readlane, no LDS
+// value of v at lane idx of this lane's instance (idx instance-uniform): v_readlane, no LDS (NP = 32: one per half)
+template <int NP>
 __device__ __forceinline__ double cs_bcast(double v, int idx)
 {
-    const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
-    const double a0 = lane_f64(v, i0), a1 = lane_f64(v, 32 + i1);
-    return (threadIdx.x & 32) ? a1 : a0;
+    if constexpr (NP == 64) {
+        return lane_f64(v, __builtin_amdgcn_readfirstlane(idx) & 63);
+    } else {
+        const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
+        const double a0 = lane_f64(v, i0), a1 = lane_f64(v, 32 + i1);
+        return (threadIdx.x & 32) ? a1 : a0;
+    }
 }
+template <int NP>
 __device__ __forceinline__ int cs_bcast_i(int v, int idx)
 {
-    const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
-    const int a0 = __builtin_amdgcn_readlane(v, i0), a1 = __builtin_amdgcn_readlane(v, 32 + i1);
-    return (threadIdx.x & 32) ? a1 : a0;
+    if constexpr (NP == 64) {
+        return __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(idx) & 63);
+    } else {
+        const int i0 = __builtin_amdgcn_readlane(idx, 0) & 31, i1 = __builtin_amdgcn_readlane(idx, 32) & 31;
+        const int a0 = __builtin_amdgcn_readlane(v, i0), a1 = __builtin_amdgcn_readlane(v, 32 + i1);
+        return (threadIdx.x & 32) ? a1 : a0;
+    }
 }
 // value at lane s of each instance (s wave-uniform)
+template <int NP>
 __device__ __forceinline__ double cs_at(double v, int s)
 {
-    const double a0 = lane_f64(v, s), a1 = lane_f64(v, 32 + s);
-    return (threadIdx.x & 32) ? a1 : a0;
+    if constexpr (NP == 64) {
+        return lane_f64(v, s);
+    } else {
+        const double a0 = lane_f64(v, s), a1 = lane_f64(v, 32 + s);
+        return (threadIdx.x & 32) ? a1 : a0;
+    }
 }
 // wave-uniform max / min of an instance-uniform count (SGPR: loops over it are scalar loops)
+template <int NP>
 __device__ __forceinline__ int cs_wmax(int v)
 {
+    if constexpr (NP == 64) return __builtin_amdgcn_readfirstlane(v);
     const int a0 = __builtin_amdgcn_readlane(v, 0), a1 = __builtin_amdgcn_readlane(v, 32);
     return a0 > a1 ? a0 : a1;
 }
+template <int NP>
 __device__ __forceinline__ int cs_wmin(int v)
 {
+    if constexpr (NP == 64) return __builtin_amdgcn_readfirstlane(v);
     const int a0 = __builtin_amdgcn_readlane(v, 0), a1 = __builtin_amdgcn_readlane(v, 32);
     return a0 < a1 ? a0 : a1;
 }
 
-// M's row (in registers) times a 32-vector in LDS: every read issued before the first FMA (one LDS round trip)
-__device__ __forceinline__ double cs_rdot(const double (&m)[32], const double *b)
+// M's row (in registers) times an NP-vector in LDS, the reads in chunks issued before their FMAs (NP = 32: all 32,
+// one LDS round trip; NP = 64: chunks of 16, the row itself already takes 128 VGPRs)
+template <int NP>
+__device__ __forceinline__ double cs_rdot(const double (&m)[NP], const double *b)
 {
-    double bv[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) bv[j] = b[j];
-    __builtin_amdgcn_sched_barrier(0);
+    constexpr int CH = NP == 64 ? 16 : 32;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < 32; ++j) s[j & 3] = fma(m[j], bv[j], s[j & 3]);
+    for (int j0 = 0; j0 < NP; j0 += CH) {
+        double bv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) bv[j] = b[j0 + j];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) s[j & 3] = fma(m[j0 + j], bv[j], s[j & 3]);
+    }
     return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
@@ -132,9 +162,10 @@ __device__ __forceinline__ double cs_gdot(const double *row, const double *vec, 
 }
 // sum_{j <= a} T[a][j] vec[j]: row a of the packed T (entries past the diagonal belong to later rows: masked;
 // vec is zero past the live slots)
+template <int KM>
 __device__ __forceinline__ double cs_trowdot(const double *tp, int a, const double *vec, int kmax)
 {
-    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
+    const int ac = a < KM ? a : KM - 1;
     const double *row = tp + ac * (ac + 1) / 2;
     double s0 = 0.0, s1 = 0.0;
     for (int j0 = 0; j0 < kmax; j0 += 8) {
@@ -154,15 +185,16 @@ __device__ __forceinline__ double cs_trowdot(const double *tp, int a, const doub
 }
 // sum_{j >= a} T[j][a] vec[j]: column a of the packed T (T finite everywhere -- zeroed at the start; vec zero
 // past the live slots)
+template <int KM>
 __device__ __forceinline__ double cs_tcol(const double *tp, int a, const double *vec, int kmax)
 {
-    const int ac = a < CsLayout::KM ? a : CsLayout::KM - 1;
+    const int ac = a < KM ? a : KM - 1;
     double s0 = 0.0, s1 = 0.0;
     for (int j0 = 0; j0 < kmax; j0 += 8) {
         double tv[8], bv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int j = j0 + u < CsLayout::KM ? j0 + u : CsLayout::KM - 1;
+            const int j = j0 + u < KM ? j0 + u : KM - 1;
             tv[u] = tp[j * (j + 1) / 2 + ac];
             bv[u] = vec[j0 + u];
         }
@@ -185,58 +217,59 @@ struct CsSlots {
 
 // Gamma[:][p] for the instance-uniform joint p: w = P m_p, c_i = M_i . w; cpp = |w|^2 = Gamma_pp. vcol: this
 // lane's column of V = Q1 M, so Q1 m_p is lane p's (no reduction)
-template <int M0>
-__device__ __forceinline__ double cs_column(double *S, const double (&mrow)[32], const double (&q1)[M0],
+template <int NP, int M0>
+__device__ __forceinline__ double cs_column(double *S, const double (&mrow)[NP], const double (&q1)[M0],
                                            const double (&vcol)[M0], int i, int p, double &cpp)
 {
     // M[i][p] = M[p][i] (a select chain: a select tree on p's bits became a dynamically indexed copy of the row
     // in scratch, 0 -> 496 B)
     double mp = 0.0;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) mp = (r == p) ? mrow[r] : mp;
+    for (int r = 0; r < NP; ++r) mp = (r == p) ? mrow[r] : mp;
     double w = mp;
 #pragma unroll
-    for (int c = 0; c < M0; ++c) w = fma(-q1[c], cs_bcast(vcol[c], p), w);
-    cpp = isum<32>(w * w);
+    for (int c = 0; c < M0; ++c) w = fma(-q1[c], cs_bcast<NP>(vcol[c], p), w);
+    cpp = isum<NP>(w * w);
     cs_order(); // (the previous readers of WV)
-    S[CsLayout::WV + i] = w;
+    S[CsLayoutT<NP>::WV + i] = w;
     cs_order();
-    return cs_rdot(mrow, S + CsLayout::WV);
+    return cs_rdot<NP>(mrow, S + CsLayoutT<NP>::WV);
 }
 
 // l = T v, r = T^T l on the slot lanes (a < cnt; v on those lanes), through VV / LV
+template <int NP>
 __device__ __forceinline__ void cs_tsolve(double *S, int i, double v, int cnt, int kmax, double &l, double &r)
 {
-    S[CsLayout::VV + i] = i < cnt ? v : 0.0;
+    S[CsLayoutT<NP>::VV + i] = i < cnt ? v : 0.0;
     cs_order();
-    l = i < cnt ? cs_trowdot(S + CsLayout::TP, i, S + CsLayout::VV, kmax) : 0.0;
-    S[CsLayout::LV + i] = l;
+    l = i < cnt ? cs_trowdot<CsLayoutT<NP>::KM>(S + CsLayoutT<NP>::TP, i, S + CsLayoutT<NP>::VV, kmax) : 0.0;
+    S[CsLayoutT<NP>::LV + i] = l;
     cs_order();
-    r = i < cnt ? cs_tcol(S + CsLayout::TP, i, S + CsLayout::LV, kmax) : 0.0;
+    r = i < cnt ? cs_tcol<CsLayoutT<NP>::KM>(S + CsLayoutT<NP>::TP, i, S + CsLayoutT<NP>::LV, kmax) : 0.0;
 }
 
 // u = u0 + P M rho, x = M u on the lanes with on set (instance-uniform); collective
-template <int M0>
-__device__ __forceinline__ void cs_rebuild(double *S, const double (&mrow)[32], const double (&q1)[M0], int i,
+template <int NP, int M0>
+__device__ __forceinline__ void cs_rebuild(double *S, const double (&mrow)[NP], const double (&q1)[M0], int i,
                                            bool on, const CsSlots &g, double u0, double &u, double &x)
 {
     cs_order();
-    S[CsLayout::VV + i] = 0.0;
+    S[CsLayoutT<NP>::VV + i] = 0.0;
     cs_order();
-    if (on && i < g.k) S[CsLayout::VV + g.act] = g.sg * g.lam;
+    if (on && i < g.k) S[CsLayoutT<NP>::VV + g.act] = g.sg * g.lam;
     cs_order();
-    const double y = cs_rdot(mrow, S + CsLayout::VV);
+    const double y = cs_rdot<NP>(mrow, S + CsLayoutT<NP>::VV);
     double vq[M0];
 #pragma unroll
     for (int c = 0; c < M0; ++c) vq[c] = q1[c] * y;
-    isum_vec<32, M0>(vq);
+    isum_vec<NP, M0>(vq);
     double py = y;
 #pragma unroll
     for (int c = 0; c < M0; ++c) py = fma(-q1[c], vq[c], py);
     const double un = u0 + py;
-    S[CsLayout::WV + i] = un;
+    S[CsLayoutT<NP>::WV + i] = un;
     cs_order();
-    const double xn = cs_rdot(mrow, S + CsLayout::WV);
+    const double xn = cs_rdot<NP>(mrow, S + CsLayoutT<NP>::WV);
     if (on) {
         u = un;
         x = xn;
@@ -257,29 +290,29 @@ constexpr double kCsDep = 1e-14;   // a row whose Schur complement is below kCsD
 // warm appends, warm multipliers, select, column, step, drop, rebuild -- and 2 counts from LAPC: passes, rebuilds)
 // VIN: vcol and x0 = M u0 are given (the fast path); else they are formed here (vcol from Q1's rows in LDS: the
 // repair)
-template <int M0, int LAPB = 0, int LAPC = 0, bool VIN = true>
+template <int NP, int M0, int LAPB = 0, int LAPC = 0, bool VIN = true>
 __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u0, int &status, int &iters,
                                            bool &infeasible, int wsg, bool record, double &u_out,
-                                           const double (&vin)[M0], bool &bail, double x0 = 0.0)
+                                           const double (&vin)[M0], bool &bail, double x0 = 0.0, int handoff = 0)
 {
-    using L = CsLayout;
+    using L = CsLayoutT<NP>;
     constexpr int KM = L::KM, GS = L::GS;
     const int n = a.n, m0 = a.m0;
     const int ic = i < n ? i : n - 1;
     WBQ_LAP_INIT;
     double q1[M0];
 #pragma unroll
-    for (int c = 0; c < M0; ++c) q1[c] = c < m0 ? S[c * 33 + i] : 0.0;
+    for (int c = 0; c < M0; ++c) q1[c] = c < m0 ? S[c * (NP + 1) + i] : 0.0;
     const double *Mb = a.M + b * n * n + ic;
-    double mrow[32];
+    double mrow[NP];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) mrow[r] = Mb[(r < n ? r : n - 1) * n];
+    for (int r = 0; r < NP; ++r) mrow[r] = Mb[(r < n ? r : n - 1) * n];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
+    for (int r = 0; r < NP; ++r) mrow[r] = (row && r < n) ? mrow[r] : (r == i ? 1.0 : 0.0);
     double nrm2 = 0.0;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) nrm2 = fma(mrow[r], mrow[r], nrm2);
+    for (int r = 0; r < NP; ++r) nrm2 = fma(mrow[r], mrow[r], nrm2);
     const double inrm = frsq(nrm2); // (the selection's scale: 1 / |M row i|)
     double vcol[M0];
     if constexpr (VIN) {
@@ -291,7 +324,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
             double v = 0.0;
             if (c < m0)
 #pragma unroll
-                for (int r = 0; r < 32; ++r) v = fma(S[c * 33 + r], mrow[r], v);
+                for (int r = 0; r < NP; ++r) v = fma(S[c * (NP + 1) + r], mrow[r], v);
             vcol[c] = v;
         }
     }
@@ -301,7 +334,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         double qq[M0];
 #pragma unroll
         for (int c = 0; c < M0; ++c) qq[c] = q1[c] * q1[c];
-        isum_vec<32, M0>(qq);
+        isum_vec<NP, M0>(qq);
         int rk = 0;
 #pragma unroll
         for (int c = 0; c < M0; ++c) rk += (c < m0 && qq[c] > 0.5) ? 1 : 0;
@@ -313,15 +346,15 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
     for (int j = 0; j < KM; ++j) S[L::GA + i * GS + j] = 0.0;
 #pragma unroll
-    for (int j = 0; j < (KM * (KM + 1) / 2 + 31) / 32; ++j)
-        if (j * 32 + i < KM * (KM + 1) / 2) S[L::TP + j * 32 + i] = 0.0;
+    for (int j = 0; j < (KM * (KM + 1) / 2 + NP - 1) / NP; ++j)
+        if (j * NP + i < KM * (KM + 1) / 2) S[L::TP + j * NP + i] = 0.0;
     double s;
     if constexpr (VIN) {
         s = x0; // the fast path's x = M u0 (the activities its bound check saw)
     } else {
         S[L::WV + i] = u0;
         cs_order();
-        s = cs_rdot(mrow, S + L::WV); // s = M u0
+        s = cs_rdot<NP>(mrow, S + L::WV); // s = M u0
     }
     double u = u0, x = s;
     CsSlots g;
@@ -333,30 +366,30 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
     if (__any(go && row && wsg != 0)) {
         const bool wme = go && row && wsg != 0;
         const unsigned long long bal = __ballot(wme);
-        unsigned rem = (unsigned)(bal >> (threadIdx.x & 32));
-        const int kw = __popc(rem);
-        const int kwmax = cs_wmax(kw);
+        unsigned long long rem = NP == 64 ? bal : ((bal >> (threadIdx.x & 32)) & 0xffffffffull);
+        const int kw = __popcll(rem);
+        const int kwmax = cs_wmax<NP>(kw);
         bool dep = kw > KM || kw > dim;
         for (int a2 = 0; a2 < kwmax; ++a2) {
             const bool on = a2 < kw && !dep;
-            const int j = rem ? __builtin_ctz(rem) : 0;
-            rem &= rem ? rem - 1u : 0u;
-            const double sj = (double)cs_bcast_i(wsg, j);
+            const int j = rem ? __builtin_ctzll(rem) : 0;
+            rem &= rem ? rem - 1ull : 0ull;
+            const double sj = (double)cs_bcast_i<NP>(wsg, j);
             double cpp;
-            const double c = cs_column<M0>(S, mrow, q1, vcol, i, j, cpp);
-            const double cg = __shfl(c, g.act, 32);
+            const double c = cs_column<NP, M0>(S, mrow, q1, vcol, i, j, cpp);
+            const double cg = __shfl(c, g.act, NP);
             const double v = (on && i < a2) ? g.sg * sj * cg : 0.0;
             double l, r;
-            cs_tsolve(S, i, v, on ? a2 : 0, a2 < KM ? a2 + 1 : KM, l, r);
-            const double d2 = cpp - isum<32>(l * l);
+            cs_tsolve<NP>(S, i, v, on ? a2 : 0, a2 < KM ? a2 + 1 : KM, l, r);
+            const double d2 = cpp - isum<NP>(l * l);
             if (on && !(d2 > kCsDep * cpp)) dep = true; // a dependent batch: start cold
             const bool on2 = on && !dep;
             const double id = d2 > 0.0 ? frsq(d2) : 0.0;
             if (on2 && i < a2) S[L::TP + a2 * (a2 + 1) / 2 + i] = -r * id;
             if (on2 && i == a2) S[L::TP + a2 * (a2 + 1) / 2 + a2] = id;
             if (on2) S[L::GA + i * GS + a2] = c;
-            const double loj = cs_bcast(lo, j), hij = cs_bcast(hi, j);
-            const bool eqj = cs_bcast_i(eqb ? 1 : 0, j) != 0;
+            const double loj = cs_bcast<NP>(lo, j), hij = cs_bcast<NP>(hi, j);
+            const bool eqj = cs_bcast_i<NP>(eqb ? 1 : 0, j) != 0;
             if (on2 && i == a2) {
                 g.act = j;
                 g.sg = sj;
@@ -368,11 +401,11 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         WBQ_LAP(1);
         // multipliers of the batch optimum from u0: K lambda = beta_W - sg_W s_W
         const int kk = dep ? 0 : kw;
-        const double xa = __shfl(s, g.act, 32);
+        const double xa = __shfl(s, g.act, NP);
         double l, lw;
-        cs_tsolve(S, i, g.beta - g.sg * xa, kk, kwmax < KM ? kwmax : KM, l, lw);
-        const double lmx = imax<32>(i < kk ? fabs(lw) : 0.0);
-        const bool bad = imax<32>((i < kk && !g.aeq && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
+        cs_tsolve<NP>(S, i, g.beta - g.sg * xa, kk, kwmax < KM ? kwmax : KM, l, lw);
+        const double lmx = imax<NP>(i < kk ? fabs(lw) : 0.0);
+        const bool bad = imax<NP>((i < kk && !g.aeq && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
         const bool keep = kk > 0 && !bad;
         S[L::RV + i] = (keep && i < kk) ? g.sg * lw : 0.0;
         cs_order();
@@ -399,11 +432,11 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
             // re-appended from their Gamma columns (GA)
             const bool dr = cdrop >= 0;
             const int cd = dr ? cdrop : 0;
-            const int cb = cs_bcast_i(g.act, cd);
+            const int cb = cs_bcast_i<NP>(g.act, cd);
             if (dr && i == cb) onact = false;
-            const int na = __shfl(g.act, i + 1, 32);
-            const double ns = __shfl(g.sg, i + 1, 32), nl = __shfl(g.lam, i + 1, 32), nb = __shfl(g.beta, i + 1, 32);
-            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1, 32) != 0;
+            const int na = __shfl(g.act, i + 1, NP);
+            const double ns = __shfl(g.sg, i + 1, NP), nl = __shfl(g.lam, i + 1, NP), nb = __shfl(g.beta, i + 1, NP);
+            const bool ne = __shfl(g.aeq ? 1 : 0, i + 1, NP) != 0;
             if (dr && i >= cd) {
                 g.act = na;
                 g.sg = ns;
@@ -416,15 +449,15 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 --g.k;
             }
             cs_order();
-            const int amin = cs_wmin(dr ? cd : KM), amax = cs_wmax(dr ? g.k : 0);
+            const int amin = cs_wmin<NP>(dr ? cd : KM), amax = cs_wmax<NP>(dr ? g.k : 0);
             for (int a2 = amin; a2 < amax; ++a2) {
                 const bool on = dr && a2 >= cd && a2 < g.k;
-                const double sa = cs_at(g.sg, a2);
+                const double sa = cs_at<NP>(g.sg, a2);
                 const double gv = S[L::GA + g.act * GS + a2]; // Gamma[act_b][act_a2]
-                const double diag = cs_at(gv, a2);
+                const double diag = cs_at<NP>(gv, a2);
                 double l, r;
-                cs_tsolve(S, i, sa * g.sg * gv, on ? a2 : 0, a2 + 1, l, r);
-                const double e2 = diag - isum<32>(l * l);
+                cs_tsolve<NP>(S, i, sa * g.sg * gv, on ? a2 : 0, a2 + 1, l, r);
+                const double e2 = diag - isum<NP>(l * l);
                 const double id = e2 > 0.0 ? frsq(e2) : 0.0;
                 if (on && i < a2) S[L::TP + a2 * (a2 + 1) / 2 + i] = -r * id;
                 if (on && i == a2) S[L::TP + a2 * (a2 + 1) / 2 + a2] = id;
@@ -442,7 +475,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 if (viol > tol) v = viol * inrm;
             }
             int pi = i;
-            iargmax<32>(v, pi);
+            iargmax<NP>(v, pi);
             if (!(v > 0.0) || recheck) {
                 recheck = false;
                 // no violated bound at these activities: optimal if they are exact, else rebuild first
@@ -450,9 +483,9 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                 if (go && !dirty) go = false;
             } else {
                 p = pi;
-                sgp = (cs_bcast(lo - s, p) > cs_bcast(s - hi, p)) ? 1.0 : -1.0;
-                bnd = sgp > 0.0 ? cs_bcast(lo, p) : cs_bcast(hi, p);
-                peq = cs_bcast_i(eqb ? 1 : 0, p) != 0;
+                sgp = (cs_bcast<NP>(lo - s, p) > cs_bcast<NP>(s - hi, p)) ? 1.0 : -1.0;
+                bnd = sgp > 0.0 ? cs_bcast<NP>(lo, p) : cs_bcast<NP>(hi, p);
+                peq = cs_bcast_i<NP>(eqb ? 1 : 0, p) != 0;
                 lamp = 0.0;
                 have_col = false;
             }
@@ -460,23 +493,23 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         WBQ_LAP(3);
         if (__any(rb)) {
             // u and x from the multipliers, refinement on the active set, then every bound re-checked
-            cs_rebuild<M0>(S, mrow, q1, i, rb, g, u0, u, x);
-            const int kmx = cs_wmax(rb ? g.k : 0);
+            cs_rebuild<NP, M0>(S, mrow, q1, i, rb, g, u0, u, x);
+            const int kmx = cs_wmax<NP>(rb ? g.k : 0);
             if (kmx > 0) {
                 for (int pass = 0; pass < 3; ++pass) {
-                    const double xa = __shfl(x, g.act, 32);
+                    const double xa = __shfl(x, g.act, NP);
                     const double res = (rb && i < g.k) ? g.beta - g.sg * xa : 0.0;
-                    const double rmx = imax<32>(rb ? fabs(res) / (1.0 + fabs(xa)) : 0.0);
+                    const double rmx = imax<NP>(rb ? fabs(res) / (1.0 + fabs(xa)) : 0.0);
                     if (!__any(rb && rmx > 1e-13)) break;
                     double l, dl;
-                    cs_tsolve(S, i, res, rb ? g.k : 0, kmx, l, dl);
+                    cs_tsolve<NP>(S, i, res, rb ? g.k : 0, kmx, l, dl);
                     if (rb && i < g.k) g.lam += dl;
-                    cs_rebuild<M0>(S, mrow, q1, i, rb, g, u0, u, x);
+                    cs_rebuild<NP, M0>(S, mrow, q1, i, rb, g, u0, u, x);
                 }
                 // every active bound must hold at the rebuilt x, else the factor is too poor: hand off
-                const double xa = __shfl(x, g.act, 32);
+                const double xa = __shfl(x, g.act, NP);
                 const double miss = (rb && i < g.k) ? fabs(g.beta - g.sg * xa) / (1.0 + fabs(xa)) : 0.0;
-                if (rb && imax<32>(miss) > 1e-8) {
+                if (rb && imax<NP>(miss) > 1e-8) {
                     bail = true;
                     go = false;
                 }
@@ -496,7 +529,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         if (!__any(go)) break;
         if (__any(go && !have_col)) { // (a drop keeps stepping on p: its column is kept)
             double cppn;
-            const double cn = cs_column<M0>(S, mrow, q1, vcol, i, p, cppn);
+            const double cn = cs_column<NP, M0>(S, mrow, q1, vcol, i, p, cppn);
             if (!have_col) {
                 c = cn;
                 cpp = cppn;
@@ -506,21 +539,21 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         WBQ_LAP(4);
         WBQ_LAP_ADD(0, 1);
         // ---- the step for bound p
-        const int k = g.k, kmx = cs_wmax(go ? k : 0);
-        const double cg = __shfl(c, g.act, 32); // Gamma[act_a][p] on slot lane a
+        const int k = g.k, kmx = cs_wmax<NP>(go ? k : 0);
+        const double cg = __shfl(c, g.act, NP); // Gamma[act_a][p] on slot lane a
         const double v = (i < k) ? g.sg * sgp * cg : 0.0;
         double l, r;
-        cs_tsolve(S, i, v, go ? k : 0, kmx, l, r);
-        const double d2 = cpp - isum<32>(l * l);
+        cs_tsolve<NP>(S, i, v, go ? k : 0, kmx, l, r);
+        const double d2 = cpp - isum<NP>(l * l);
         S[L::RV + i] = (go && i < k) ? g.sg * r : 0.0;
         cs_order();
         const double ds = sgp * c - cs_gdot(S + L::GA + i * GS, S + L::RV, kmx);
-        const double zz = sgp * cs_bcast(ds, p);
-        const double slack = sgp * (cs_bcast(s, p) - bnd); // < 0: violated
-        const double rmax = imax<32>(i < k ? fabs(r) : 0.0);
+        const double zz = sgp * cs_bcast<NP>(ds, p);
+        const double slack = sgp * (cs_bcast<NP>(s, p) - bnd); // < 0: violated
+        const double rmax = imax<NP>(i < k ? fabs(r) : 0.0);
         double cand = (i < k && !g.aeq && r > 1e-13 * rmax) ? g.lam * frcp(r) : kInf;
         int ci = i;
-        iargmin<32>(cand, ci);
+        iargmin<NP>(cand, ci);
         const double t1 = cand;
         const double t2 = (k < dim && d2 > kCsDep * cpp && zz > 0.0) ? -slack * frcp(zz) : kInf;
         if (go) {
@@ -567,6 +600,13 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
                     status = 1;
                     go = false;
                 }
+                // handoff > 0: a loop still running after that many steps goes to the level-0 repair as if
+                // infeasible (its BVLS settles level 0 first; a feasible instance comes back unpinned: the same
+                // result), as gi_solve's
+                if (handoff > 0 && iters >= handoff && go) {
+                    infeasible = true;
+                    go = false;
+                }
             }
         }
         WBQ_LAP(5);
@@ -588,7 +628,7 @@ __device__ __forceinline__ double cs_solve(const QppvmArgs &a, double *S, long b
         cs_order();
 #pragma unroll
         for (int c = 0; c < M0; ++c)
-            if (bail && c < m0) S[c * 33 + i] = q1[c];
+            if (bail && c < m0) S[c * (NP + 1) + i] = q1[c];
         cs_order();
     }
     u_out = u;

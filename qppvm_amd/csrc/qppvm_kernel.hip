@@ -609,6 +609,9 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         WBQ_STAMP(6);
         const bool warm_gi = valid && (PIN || (a.ws_hint[b] & 2));
         const int wsg = (warm_gi && row) ? (int)a.ws_rows[b * 64 + i] : 0;
+        // (round 6: the constraint-space loop of cs_gi.h at 64 lanes here -- Gamma columns over n <= 64 rows, T = L^-1
+        // over the QA region, a hand-off to this u-space loop -- ended 3 of 96 heavily saturated n = 39 instances of
+        // tests/test_gpu_handback.py at the step cap (4 n + 32) where this loop converges: not used for n > 32)
         const double x_i = gi_solve<NP, M0, PIN ? 48 : 32, PIN ? 56 : 40>(a, S, b, i, row, valid, lo, hi,
                                                                         valid ? a.u_scr[b * NP + i] : 0.0, status,
                                                                         iters, infeasible, wsg, true,
@@ -719,7 +722,7 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
             bool bail;
             double uo;
             const double vnone[M0] = {};
-            x_i = cs_solve<M0, 48, 56, false>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr,
+            x_i = cs_solve<NP, M0, 48, 56, false>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr,
                                               true, uo, vnone, bail);
             if (__any(bail)) {
                 int st3 = 0, it3 = 0;
@@ -1641,7 +1644,7 @@ __device__ __forceinline__ void fast_body(const QppvmArgs &a)
                     vcol[c] = v * il[c];
                 }
                 bool bail;
-                x2 = cs_solve<M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2,
+                x2 = cs_solve<NP, M0, 20, 13>(a, S, ga ? b : 0, i, row && ga, ga, lo, hi, u_i, st2, it2, inf, wsg, true, u2,
                                           vcol, bail, x_i);
                 inf |= bail; // (the level-0 repair takes a hand-off: its u-space loop settles it)
             } else {
