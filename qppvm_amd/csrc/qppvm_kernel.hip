@@ -182,25 +182,56 @@ __device__ __forceinline__ bool go_rec(bool row, long, const QppvmArgs &a) { ret
 // (the second pass runs for the whole wave when any taking part needs it: barriers stay uniform).
 // (Each pass is two LDS dot products per lane: with eight waves per CU in this loop the LDS port is
 // the bound, and the second pass was half of it.)
+// sum_{j < cnt} a[j stride] b[j] with a wave-uniform bound (rounded up to chunks of eight reads issued together;
+// the entries past cnt are zero in the callers' data, so no masks): NP = 64 only, where one instance is the wave
+__device__ __forceinline__ double dotw(const double *a, int stride, const double *b, int cnt)
+{
+    double s0 = 0.0, s1 = 0.0;
+    for (int j0 = 0; j0 < cnt; j0 += 8) {
+        double av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            av[u] = a[(j0 + u) * stride];
+            bv[u] = b[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 = fma(av[u], bv[u], s0);
+            s1 = fma(av[u + 1], bv[u + 1], s1);
+        }
+    }
+    return s0 + s1;
+}
+
 template <int NP>
 __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> &L, double npj, int q, int i,
-                                              double nn2, bool act, double &zz)
+                                              double nn2, bool act, double &zz, int n = NP)
 {
     constexpr int RS = NP + 1;
     // (measured, round 6: the LDS reads of these dots issued a chunk ahead -- dot4p / dot4sp, wbq_device.h --
     // spilled the n <= 32 fast kernel that inlines this loop, 0 -> ~300 B of scratch even at 4-element chunks)
-    const double d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
+    // NP = 64 (one instance per wave, q and n wave-uniform): a basis row past n and D1 past q are zero, so the dots
+    // stop there (n = 39: 40 of 64 entries; q = m0 + k rows of Q1^T) instead of running to NP
+    const int nq = NP == 64 ? (q + 7) & ~7 : NP, nn = NP == 64 ? (n + 7) & ~7 : NP;
+    double d1 = 0.0;
+    if constexpr (NP == 64) d1 = i < q ? dotw(S + L.QA + i * RS, 1, S + L.NV, nn) : 0.0;
+    else d1 = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.NV) : 0.0;
     S[L.D1 + i] = d1;
     gs_sync();
-    double z = npj - dot4s<NP>(S + L.QA + i, RS, S + L.D1);
+    double z;
+    if constexpr (NP == 64) z = npj - dotw(S + L.QA + i, RS, S + L.D1, nq);
+    else z = npj - dot4s<NP>(S + L.QA + i, RS, S + L.D1);
     zz = isum<NP>(z * z);
     if (__any(act && !(zz > 0.5 * nn2))) {
         S[L.BC + i] = z;
         gs_sync();
-        const double d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
+        double d1b;
+        if constexpr (NP == 64) d1b = i < q ? dotw(S + L.QA + i * RS, 1, S + L.BC, nn) : 0.0;
+        else d1b = i < q ? dot4<NP>(S + L.QA + i * RS, S + L.BC) : 0.0;
         S[L.D1B + i] = d1b;
         gs_sync();
-        z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
+        if constexpr (NP == 64) z -= dotw(S + L.QA + i, RS, S + L.D1B, nq);
+        else z -= dot4s<NP>(S + L.QA + i, RS, S + L.D1B);
         S[L.D1 + i] = d1 + d1b;
         zz = isum<NP>(z * z);
         gs_sync();
@@ -300,10 +331,10 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             gs_sync();
             const double npn = __shfl(nrm, pa, NP);
             double zzr;
-            const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr);
+            const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr, n);
             if (on && !(zzr > 1e-16 * npn * npn)) dep = true; // a dependent batch: start cold
             double rr2 = 0.0;
-            if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
+            if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP == 64 ? a2 : NP);
             if (on) {
                 const double iz = zzr > 0.0 ? frsq(zzr) : 0.0;
                 S[L.QA + q * (NP + 1) + i] = zr * iz;
@@ -315,7 +346,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         }
         WBQ_LAP(1);
         // residuals r_a = beta_a - n_a . u on the slot lanes, w = T^T r (lane j: w_j), lambda = T w
-        const double s0 = Mr.dot(S + L.U, NP);
+        const double s0 = Mr.dot(S + L.U, NP == 64 ? n : NP);
         const double xp = __shfl(s0, myp, NP), lop = __shfl(lo, myp, NP), hip = __shfl(hi, myp, NP);
         const int sp = __shfl(wsg, myp, NP);
         const double r = i < kw ? (sp > 0 ? lop - xp : xp - hip) : 0.0; // sgn (bound - x)
@@ -329,7 +360,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         }
         S[L.BC + i] = i < kw ? w_own : 0.0;
         gs_sync();
-        const double lw = i < kw ? Tr.dot(S + L.BC, NP) : 0.0;
+        const double lw = i < kw ? Tr.dot(S + L.BC, NP == 64 ? kw : NP) : 0.0;
         const bool peqw = __shfl(eqb ? 1 : 0, myp, NP) != 0;
         const double lmx = imax<NP>(fabs(lw));
         dep |= imax<NP>((i < kw && !peqw && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
@@ -357,7 +388,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         WBQ_LAP(2);
     }
     while (true) {
-        const double s_i = Mr.dot(S + L.U, NP); // s = M u = x
+        const double s_i = Mr.dot(S + L.U, NP == 64 ? n : NP); // s = M u = x
         if (need_select) {
             double v = -1.0;
             if (row) {
@@ -383,10 +414,10 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         gs_sync();
         WBQ_LAP(3);
         double zz;
-        const double z = project_out<NP>(S, L, npj, q, i, npn * npn, go, zz);
+        const double z = project_out<NP>(S, L, npj, q, i, npn * npn, go, zz, n);
         WBQ_LAP(4);
         double ra = 0.0;
-        if (i < k) ra = Tr.dot(S + L.D1 + m0, NP);
+        if (i < k) ra = Tr.dot(S + L.D1 + m0, NP == 64 ? k : NP);
         const double rmax = imax<NP>(fabs(ra));
         // equality rows (pinned or lo == hi) are never dropped
         double cand = (i < k && !act_e && ra > 1e-13 * rmax) ? lam / ra : kInf;
@@ -531,9 +562,9 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
                 gs_sync();
                 const double npa = __shfl(nrm, pa, NP);
                 double zzr;
-                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npa * npa, on, zzr);
+                const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npa * npa, on, zzr, n);
                 double rr2 = 0.0;
-                if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP);
+                if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP == 64 ? a2 : NP);
                 if (on) {
                     const double iz = frsq(zzr);
                     S[L.QA + q * RS + i] = zr * iz;
@@ -559,7 +590,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         if (go_rec(row, b, a)) a.ws_rows[b * 64 + i] = (signed char)(ok ? (sgn > 0.0 ? 1 : (sgn < 0.0 ? -1 : 0)) : 0);
         gs_sync();
     }
-    const double xf = Mr.dot(S + L.U, NP);
+    const double xf = Mr.dot(S + L.U, NP == 64 ? n : NP);
     WBQ_LAP(7);
     if constexpr (LAPB > 0) WBQ_LAP_FLUSH(LAPB, LAPC);
     return xf;
