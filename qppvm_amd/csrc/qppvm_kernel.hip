@@ -616,7 +616,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         const long e = e0 + sub;
         const bool valid = e < cnt;
         WBQ_STAMP(4);
-        WBQ_RTSTAMP(30);
+        WBQ_RTSTAMP(PIN ? 42 : 30); // (diagnostic: the hand-back pass keeps its own realtime slots, 42-43)
         const long b = valid ? a.wl[(PIN ? 2 * a.B : 0) + e] : 0;
         const int n = a.n;
         const bool row = valid && i < n;
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
             }
         }
         WBQ_STAMP(7);
-        WBQ_RTSTAMP(31);
+        WBQ_RTSTAMP(PIN ? 43 : 31);
     }
 }
 

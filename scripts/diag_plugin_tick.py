@@ -52,24 +52,35 @@ def main():
         assert s.lib.wbq_diag_stamps(s.ctx, buf, 1) == 0
         st = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
         tau, status, iters = s.outputs()
-        rep = st[12] > st[8]
-        row = {"tick": t, "us": 1e3 * ms, "status": int(status[0]), "iters": int(iters[0]), "repair": bool(rep),
-               "fast_cycles": int(st[5] - st[0])}
-        # the constant 100 MHz clock (s_memrealtime, global): where the tick's device time goes, and the
-        # shader clock each phase ran at (s_memtime cycles / realtime)
-        t0 = st[16]
-        row["rt_us"] = {"fast": (st[17] - st[16]) / 100.0}
+        # the repair kernel ran for this instance when its realtime stamps are set (a repair that hands its level-1
+        # loop back returns before stamp 12, so "st[12] > st[8]" missed exactly the hand-back ticks)
+        rep = bool(st[29] > st[28] > 0)
+        hb = bool(st[43] > st[42] > 0)
+        row = {"tick": t, "us": 1e3 * ms, "status": int(status[0]), "iters": int(iters[0]), "repair": rep,
+               "handback": hb, "fast_cycles": int(st[5] - st[0])}
+        # the constant 100 MHz clock (s_memrealtime, global): each launch's own span (fast kernel 16-17, active-set
+        # kernel 30-31, repair kernel 28-29, hand-back pass 42-43) and the gaps between consecutive launches
+        spans = [("fast", 16, 17)]
         if st[31] > st[30] > 0:
-            row["rt_us"]["active"] = (st[31] - st[30]) / 100.0
-            row["rt_us"]["fast_end_to_active"] = (st[30] - st[17]) / 100.0
-        if rep and st[29] > st[28] > 0:
-            row["rt_us"]["repair"] = (st[29] - st[28]) / 100.0
-            row["rt_us"]["before_repair"] = (st[28] - (st[31] if st[31] > st[30] > 0 else st[17])) / 100.0
-            row["rt_us"]["span"] = (st[29] - t0) / 100.0
-            row["repair_clock_ghz"] = (st[12] - st[8]) / max(1.0, (st[29] - st[28]) / 100.0) / 1e3
+            spans.append(("active", 30, 31))
+        if rep:
+            spans.append(("repair", 28, 29))
+            row["repair_clock_ghz"] = (st[12] - st[8]) / max(1.0, (st[29] - st[28]) / 100.0) / 1e3 if st[12] > st[8] \
+                else (st[11] - st[8]) / max(1.0, (st[29] - st[28]) / 100.0) / 1e3
+        if hb:
+            spans.append(("handback", 42, 43))
+        row["rt_us"] = {}
+        prev_end = None
+        for nm, a0, a1 in spans:
+            if prev_end is not None:
+                row["rt_us"]["gap_before_" + nm] = (st[a0] - prev_end) / 100.0
+            row["rt_us"][nm] = (st[a1] - st[a0]) / 100.0
+            prev_end = st[a1]
+        row["rt_us"]["span"] = (prev_end - st[16]) / 100.0
         row["fast_clock_ghz"] = (st[5] - st[0]) / max(1.0, (st[17] - st[16]) / 100.0) / 1e3
-        # the dual loop's lap counters (gi_solve): active-set kernel slots 32-41, repair kernel 48-57
-        for nm, base, cb in (("active_gi", 32, 40), ("repair_gi", 48, 56)):
+        # the dual loop's lap counters (gi_solve): active-set kernel slots 32-41; 48-57 the pinned level 1's loop,
+        # in the hand-back pass or (hand-back off) in the repair kernel
+        for nm, base, cb in (("active_gi", 32, 40), ("pinned_gi", 48, 56)):
             laps = [int(v) for v in st[base:base + 8]]
             if sum(laps) > 0:
                 passes = int(st[cb])
@@ -78,23 +89,23 @@ def main():
                            "laps_setup_warm_wstep_select_proj_step_rebuild_rec": laps}
         if rep:
             row.update({"gj": int(st[9] - st[8]), "bvls": int(st[10] - st[9]), "pins_eq": int(st[11] - st[10]),
-                        "gi": int(st[12] - st[11]), "bvls_it": int(st[13]), "gi_it": int(st[14]),
-                        "bvls_split": [int(v) for v in st[20:28]]})
+                        "bvls_it": int(st[13]), "bvls_split": [int(v) for v in st[20:28]]})
+            if st[12] > st[11]:  # (the level-1 loop ran inside the repair kernel, not in the hand-back pass)
+                row.update({"gi": int(st[12] - st[11]), "gi_it": int(st[14])})
         rows.append(row)
     s.close()
     json.dump(rows, open(out, "w"), indent=1)
     us = np.array([r["us"] for r in rows])
-    print(json.dumps({"ticks": ticks, "us_p50_p90_p99_max": [float(np.percentile(us, q)) for q in (50, 90, 99, 100)],
-                      "repair_share": float(np.mean([r["repair"] for r in rows]))}))
-    # stamped time vs device time: the share of each tick the realtime stamps account for
-    acc = [sum(v for k, v in r["rt_us"].items() if k in ("fast", "active", "repair", "fast_end_to_active", "before_repair"))
-           / r["us"] for r in rows if r["repair"] and "repair" in r["rt_us"]]
-    if acc:
-        print(json.dumps({"repaired_ticks": len(acc), "realtime_span_over_device_time_p10_p50_p90":
-                          [float(np.percentile(acc, q)) for q in (10, 50, 90)],
-                          "repair_clock_ghz_p10_p50_p90": [float(np.percentile([r["repair_clock_ghz"] for r in rows
-                                                                                 if "repair_clock_ghz" in r], q))
-                                                           for q in (10, 50, 90)]}))
+    print(json.dumps({"ticks": ticks, "us_p50_p90_p99_max": [float(np.percentile(us, q)) for q in (50, 90, 99, 100)]}))
+    # stamped time vs device time: the share of each tick its launches' spans and the gaps between them account for
+    # (every tick, the slowest included; the rest of a tick's device time is the first launch's dispatch)
+    acc = [r["rt_us"]["span"] / r["us"] for r in rows]
+    slow = sorted(rows, key=lambda r: -r["us"])[:8]
+    print(json.dumps({"ticks_stamped": len(acc), "span_over_device_time_p10_p50_p90":
+                      [float(np.percentile(acc, q)) for q in (10, 50, 90)],
+                      "slowest8_span_over_device_time": [round(r["rt_us"]["span"] / r["us"], 3) for r in slow],
+                      "repair_share": float(np.mean([r["repair"] for r in rows])),
+                      "handback_share": float(np.mean([r["handback"] for r in rows]))}))
     for r in sorted(rows, key=lambda r: -r["us"])[:8]:
         print(json.dumps(r))
 
