@@ -400,15 +400,16 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             iargmax<NP>(v, pi);
             if (!(v > 0.0)) go = false; // optimal
             p = pi;
-            sg = (__shfl(lo - s_i, p, NP) > __shfl(s_i - hi, p, NP)) ? 1 : -1;
+            // (p is instance-uniform: v_readlane broadcasts, no ds_bpermute round trips)
+            sg = (cs_bcast<NP>(lo - s_i, p) > cs_bcast<NP>(s_i - hi, p)) ? 1 : -1;
             lamp = 0.0;
         }
         if (!__any(go)) break;
         WBQ_LAP_ADD(0, 1);
-        const double s_p = __shfl(s_i, p, NP);
-        const double sp = sg > 0 ? s_p - __shfl(lo, p, NP) : __shfl(hi, p, NP) - s_p; // slack < 0
-        const double npn = __shfl(nrm, p, NP);
-        const bool peq = __shfl(eqb ? 1 : 0, p, NP) != 0;
+        const double s_p = cs_bcast<NP>(s_i, p);
+        const double sp = sg > 0 ? s_p - cs_bcast<NP>(lo, p) : cs_bcast<NP>(hi, p) - s_p; // slack < 0
+        const double npn = cs_bcast<NP>(nrm, p);
+        const bool peq = cs_bcast_i<NP>(eqb ? 1 : 0, p) != 0;
         const double npj = sg * Mr.get(p); // n_p = sg * M row p (M symmetric)
         S[L.NV + i] = npj;
         gs_sync();
@@ -496,9 +497,13 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             // per rotation, where re-projecting every later normal cost two to four LDS dot products each
             // (the stress plant's n = 39 dual loops spent ~60 % of their cycles there, scripts/diag_plugin_tick.py).
             const int kold = k + 1; // (the drop above decremented k)
+            // (one instance per wave here: kold and cdrop are wave-uniform, and T's entries past kold are zero, so
+            // the row copies below stop at kold -- they ran over all 64 columns, ~24k cycles per drop in the
+            // stress plant's hand-back loop, profiles/r06_v14_diag_tick_stress.log)
             if (rebuild && i == cdrop) {
 #pragma unroll
-                for (int j = 0; j < NP; ++j) S[L.BC + j] = Tr.at(j); // row c of T, every lane reads it
+                for (int j = 0; j < NP; ++j)
+                    if (j < kold) S[L.BC + j] = Tr.at(j); // row c of T, every lane reads it
             }
             gs_sync();
             double xr = rebuild ? S[L.BC + cdrop] : 0.0; // the chase's running entry
@@ -526,14 +531,17 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             const int nxt = i + 1 < NP ? i + 1 : i;
             {
                 double nrow[NP];
+                const int kw = cs_wmax<NP>(rebuild ? kold : 0);
 #pragma unroll
-                for (int j = 0; j < NP; ++j) nrow[j] = __shfl(Tr.at(j), nxt, NP);
+                for (int j = 0; j < NP; ++j) nrow[j] = j < kw ? __shfl(Tr.at(j), nxt, NP) : 0.0;
                 gs_sync(); // (T rows in LDS: every read of row i + 1 before its owner writes it)
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
-                    double v = (rebuild && i >= cdrop) ? nrow[j] : Tr.at(j);
-                    if (rebuild && (j >= k || i >= k)) v = 0.0; // the last column and the dead rows
-                    if (rebuild) Tr.set(j, v);
+                    if (j < kw) {
+                        double v = (rebuild && i >= cdrop) ? nrow[j] : Tr.at(j);
+                        if (rebuild && (j >= k || i >= k)) v = 0.0; // the last column and the dead rows
+                        if (rebuild) Tr.set(j, v);
+                    }
                 }
             }
             if (rebuild) q = m0 + k;
