@@ -259,7 +259,8 @@ __device__ __forceinline__ double project_out(double *S, const ActiveLayout<NP> 
 template <int NP, int M0, int LAPB = 0, int LAPC = 0>
 __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b, int i, bool row, bool go,
                                            double lo, double hi, double u_i, int &status, int &iters,
-                                           bool &infeasible, int wsg = 0, bool record = false, int handoff = 0)
+                                           bool &infeasible, int wsg = 0, bool record = false, int handoff = 0,
+                                           bool skipdep = false)
 {
     constexpr int RS = NP + 1;
     constexpr bool MREG = ActiveLayout<NP>::MREG;
@@ -320,11 +321,15 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) kwmax = max(kwmax, __shfl_xor(kwmax, m, 64));
         gs_sync();
-        const int myp = i < kw ? (int)S[L.BC + i] : 0; // this slot lane's joint
+        const int myp0 = i < kw ? (int)S[L.BC + i] : 0; // the a-th warm bound's joint on lane a
         bool dep = false;
+        // skipdep (warm sets from a level-0 repair: its BVLS bound set holds the pins, dependent on G u = y* by
+        // construction): a dependent member is left out of the batch instead of rejecting it -- it is implied by
+        // the others, so it holds at the batch optimum. Else a dependent member sends the batch cold.
+        int kk = 0, myp = 0; // members kept (instance-uniform), this slot lane's joint
         for (int a2 = 0; a2 < kwmax; ++a2) {
             const bool on = a2 < kw;
-            const int pa = on ? __shfl(myp, a2, NP) : 0; // (project_out overwrites BC)
+            const int pa = on ? __shfl(myp0, a2, NP) : 0; // (project_out overwrites BC)
             const int sa = __shfl(wsg, pa, NP);
             const double nj = on ? sa * Mr.get(pa) : 0.0;
             S[L.NV + i] = nj;
@@ -332,51 +337,60 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             const double npn = __shfl(nrm, pa, NP);
             double zzr;
             const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr, n);
-            if (on && !(zzr > 1e-16 * npn * npn)) dep = true; // a dependent batch: start cold
+            const bool indep = zzr > 1e-16 * npn * npn;
+            if (on && !indep && !skipdep) dep = true; // a dependent batch: start cold
+            const bool add = on && (indep || !skipdep);
             double rr2 = 0.0;
-            if (on && i < a2) rr2 = Tr.dot(S + L.D1 + m0, NP == 64 ? a2 : NP);
-            if (on) {
+            if (add && i < kk) rr2 = Tr.dot(S + L.D1 + m0, NP == 64 ? kk : NP);
+            if (add) {
                 const double iz = zzr > 0.0 ? frsq(zzr) : 0.0;
                 S[L.QA + q * (NP + 1) + i] = zr * iz;
-                if (i < a2) Tr.set(a2, -rr2 * iz);
-                if (i == a2) Tr.set(a2, iz);
+                if (i < kk) Tr.set(kk, -rr2 * iz);
+                if (i == kk) {
+                    Tr.set(kk, iz);
+                    myp = pa;
+                }
                 ++q;
+                ++kk;
             }
             gs_sync();
         }
+        int kkmax = kk;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) kkmax = max(kkmax, __shfl_xor(kkmax, m, 64));
         WBQ_LAP(1);
         // residuals r_a = beta_a - n_a . u on the slot lanes, w = T^T r (lane j: w_j), lambda = T w
         const double s0 = Mr.dot(S + L.U, NP == 64 ? n : NP);
         const double xp = __shfl(s0, myp, NP), lop = __shfl(lo, myp, NP), hip = __shfl(hi, myp, NP);
         const int sp = __shfl(wsg, myp, NP);
-        const double r = i < kw ? (sp > 0 ? lop - xp : xp - hip) : 0.0; // sgn (bound - x)
+        const double r = i < kk ? (sp > 0 ? lop - xp : xp - hip) : 0.0; // sgn (bound - x)
         double w_own = 0.0;
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
-            if (j < kwmax) {
-                const double t = isum<NP>(i < kw ? Tr.at(j) * r : 0.0);
+            if (j < kkmax) {
+                const double t = isum<NP>(i < kk ? Tr.at(j) * r : 0.0);
                 w_own = i == j ? t : w_own;
             }
         }
-        S[L.BC + i] = i < kw ? w_own : 0.0;
+        S[L.BC + i] = i < kk ? w_own : 0.0;
         gs_sync();
-        const double lw = i < kw ? Tr.dot(S + L.BC, NP == 64 ? kw : NP) : 0.0;
+        const double lw = i < kk ? Tr.dot(S + L.BC, NP == 64 ? kk : NP) : 0.0;
         const bool peqw = __shfl(eqb ? 1 : 0, myp, NP) != 0;
         const double lmx = imax<NP>(fabs(lw));
-        dep |= imax<NP>((i < kw && !peqw && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
+        dep |= imax<NP>((i < kk && !peqw && lw < -1e-12 * (1.0 + lmx)) ? 1.0 : 0.0) > 0.0;
         dep = imax<NP>(dep ? 1.0 : 0.0) > 0.0; // instance-uniform
-        if (kw > 0 && !dep) { // keep: step to the batch optimum, slots take the batch
+        if (kk > 0 && !dep) { // keep: step to the batch optimum, slots take the batch
             double du = 0.0;
-            for (int c = 0; c < kwmax; ++c)
-                if (c < kw) du = fma(S[L.QA + (m0 + c) * (NP + 1) + i], S[L.BC + c], du);
+            for (int c = 0; c < kkmax; ++c)
+                if (c < kk) du = fma(S[L.QA + (m0 + c) * (NP + 1) + i], S[L.BC + c], du);
             u_i += du;
-            if (i < kw) {
+            if (i < kk) {
                 act_p = myp;
                 act_s = sp;
                 act_e = peqw;
                 lam = peqw ? lw : fmax(lw, 0.0);
             }
-            k = kw;
+            k = kk;
             iters += 1;
         } else { // cold: drop the batch (rows of Q1 past m0 and T are rewritten before they are read)
             Tr.zero();
@@ -654,7 +668,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         const double x_i = gi_solve<NP, M0, PIN ? 48 : 32, PIN ? 56 : 40>(a, S, b, i, row, valid, lo, hi,
                                                                         valid ? a.u_scr[b * NP + i] : 0.0, status,
                                                                         iters, infeasible, wsg, true,
-                                                                        PIN ? 0 : a.gi_handoff);
+                                                                        PIN ? 0 : a.gi_handoff, PIN);
         if constexpr (PIN) { // (the repair kernel's epilogue)
             if (infeasible && status == 0) status = 2;
             double tau_i = x_i + h_i;
@@ -767,7 +781,7 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
                 int st3 = 0, it3 = 0;
                 bool inf3 = false;
                 const double x3 = gi_solve<NP, M0>(a, S, b, i, row && bail, bail, ro.lo, ro.hi, ro.u, st3, it3, inf3, wsr,
-                                                   true);
+                                                   true, 0, true);
                 if (bail) {
                     x_i = x3;
                     status = st3;
@@ -779,7 +793,8 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
             if (!bail) S[L.U + i] = uo; // (rollout_step below reads u there; gi_solve wrote every lane's)
             __syncthreads();
         } else {
-            x_i = gi_solve<NP, M0, 48, 56>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr, true);
+            x_i = gi_solve<NP, M0, 48, 56>(a, S, b, i, row, g1, ro.lo, ro.hi, ro.u, status, iters, infeasible, wsr, true, 0,
+                                           true);
         }
     }
     if (uniq) x_i = ro.x;
