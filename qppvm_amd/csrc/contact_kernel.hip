@@ -385,7 +385,7 @@ __device__ int contact_level0(const ContactArgs &a, long b, double *S, const Con
 #pragma unroll
         for (int r = 0; r < 6; ++r) w[r] = qrow ? w[r] : 0.0;
     }
-    __syncthreads();
+    wave_sync();
     (void)block_gj<NQ, 6, 6>(A, w, n, i, S + L.PN, S + L.RH);
     // b = b_w + W^T h (the waist targets are the waist rows' limits)
     double bv[6], hw[6];
@@ -605,7 +605,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (it * 64 + i < 24 * (1 + nc)) S[L.PS + it * 64 + i] = pv[it];
     if (i < 6 * (1 + nc)) S[L.JD + i] = jd;
     if constexpr (kMLate) lds_barrier(); // (LDS only: M keeps streaming in)
-    else __syncthreads();
+    else wave_sync();
     WBQ_STAMP(1);
 
     // ------------------------------------------------- 2. task targets (one lane per row)
@@ -620,7 +620,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         S[L.BT + i] = Kp * e - Kd * xd - S[L.JD + i];
     }
     if constexpr (kMLate) lds_barrier();
-    else __syncthreads();
+    else wave_sync();
 
     // ------------------------------- 3. H row i = e_i + sum_c J_c^T J_c row i, gradient
     double A[NQ];
@@ -669,7 +669,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
             else if (s == L.NJ + 6) v = mg;
             rhs[m] = qrow ? v : 0.0;
         }
-        __syncthreads();
+        wave_sync();
         notspd |= block_gj<NQ, NRC, NRC>(A, rhs, n, i, S + L.PN, S + L.RH);
         if (i < NQ) {
 #pragma unroll
@@ -677,7 +677,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
                 if (c0 + m < L.NR) S[L.XT + (c0 + m) * L.QS + i] = rhs[m];
         }
     }
-    __syncthreads();
+    wave_sync();
     {
         const double x0 = qrow ? S[L.XT + (L.NJ + 6) * L.QS + i] : 0.0;
         S[L.X0 + i] = x0;
@@ -765,7 +765,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
 #pragma unroll
         for (int j = 0; j < NQ; ++j) s_i = fma(aq[j], S[L.X0 + j], s_i);
     }
-    __syncthreads();
+    wave_sync();
     if (kind != 0) nrm = sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300));
     WBQ_STAMP(4);
     int it0 = 0;
@@ -776,7 +776,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     (void)kind_free;
     if constexpr (REPAIR) { // level 0 not attainable at b_w: y0* and the pins first
         if (!notspd && !a.limits_crossed) it0 = contact_level0<NQ, FR>(a, b, S, L, i, h_i, lo, hi, l0cap, wkeep);
-        __syncthreads();
+        wave_sync();
     }
     const double lo_rep = lo, hi_rep = hi; // the pinned level 1 (the QR fallback's problem)
     const int wkeep_rep = wkeep;
@@ -814,7 +814,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         }
         wkeep = 0x3f;
         s_i = s_x0;
-        __syncthreads();
+        wave_sync();
     }
     if constexpr (REPAIR) kind = (ci >= NJ && ci < NJ + 6 && !((wkeep >> (ci - NJ)) & 1)) ? 0 : kind_free;
     // batch row c: the dynamic-feasibility rows, then the kept waist rows; nb of them (12 but
@@ -893,14 +893,14 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         const double ye = __shfl(lo - s_i, er); // e_E - s_E (every lane active: sources up to lane NJ + 5)
         if (i < 12) S[L.VV + i] = i < nb ? ye : 0.0;
         S[L.AC + i] = (double)er; // slots 0..nb-1 (the gathered Gamma columns of the LDS variant)
-        __syncthreads();
+        wave_sync();
         if constexpr (SREG) Trow.load_if(i < nb, S + L.TT + (i < nb ? i : 0) * L.TS, nb);
         const double w = i < nb ? Trow.dot(S + L.VV, nb) : 0.0;
         S[L.LV + i] = w;
-        __syncthreads();
+        wave_sync();
         const double lm = i < nb ? Tcol.dot(S + L.LV, nb) : 0.0; // lambda_E
         S[L.RV + i] = lm;
-        __syncthreads();
+        wave_sync();
 #pragma unroll
         for (int q = 0; q < 12; ++q)
             GA.put(q, kind != 0, (kind != 0 && q < nb) ? S[L.GM + ci * L.GS + brow(q)] : 0.0);
@@ -914,7 +914,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         gs.k = nb;
         gs.iters = 1;
         if (sing) gs.status = 3; // dependent equality rows: the spec's level 1 is ill-posed
-        __syncthreads();
+        wave_sync();
     }
     WBQ_STAMP(9); // (diagnostic build: the equality batch ends here)
     if constexpr (!REPAIR) { // the last solve's active inequality rows on top (dual_gi.h warm_extend)
@@ -937,7 +937,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
         if (status != 0 && a.qr_fallback && !notspd && !a.limits_crossed && !l0cap) {
             const int kp = (ci >= NJ && ci < NJ + 6 && !((wkeep_rep >> (ci - NJ)) & 1)) ? 0 : kind_free;
             if (i < L.NX) S[L.XV + i] = i < n ? S[L.X0 + i] : 0.0;
-            __syncthreads();
+            wave_sync();
             const int dim = n + WD * __popc((unsigned)cm & ((1u << nc) - 1u));
             ContactGi<NQ, TR, NFM, FR> gi{S, &L, n, nf, i, ieps, dim};
             if constexpr (TR) {
@@ -949,7 +949,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
             int itq = 0;
             status = qr_gi(pq, S + L.XV, S + L.SIZE, Q, L.NX, i, kp, lo_rep, hi_rep, 10 * (L.NX + ME) + 50, itq);
             iters += itq;
-            __syncthreads();
+            wave_sync();
         }
     }
     if constexpr (!REPAIR) {
@@ -969,7 +969,7 @@ __device__ __forceinline__ void contact_solve(const ContactArgs &a, const long b
     }
 
     // ------------------------------------------------------------------ 7. outputs
-    __syncthreads();
+    wave_sync();
     WBQ_STAMP(5);
     const bool ok = status == 0;
     if (a.ws_rows) { // the next solve's warm start: this solve's final active set (a repaired solve's
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(64, 1) void contact_repair_kernel(const ContactArgs
     }
     follow_publish(a.fg, 0, cnt);
     for (long e = blockIdx.x; e < cnt; e += gridDim.x) {
-        __syncthreads(); // the previous instance's LDS is dead
+        wave_sync(); // the previous instance's LDS is dead
         contact_solve<NQ, TR, KMR, WD, true>(a, uniform_long(a.wl[e]));
     }
 }

@@ -206,7 +206,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         for (int r = 0; r < NQ; ++r)
             if (r < n) S[L.GM + (m0 + i) * L.GS + m0 + r] = mn ? (r == i ? 1.0 : 0.0) : A[r];
     }
-    __syncthreads();
+    wave_sync();
     // task-space force per task row (spring + damper, zero desired twist), QPPVMPlugin.cpp:136-137
     if (i < T * 6) {
         const int t = i / 6, r = i - t * 6;
@@ -230,7 +230,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
                 S[L.GM + c * L.GS + m0 + i] = gc[c];
             }
     }
-    __syncthreads();
+    wave_sync();
     if (i < NQ) { // J_t^T F_t (joint i)
 #pragma unroll
         for (int t = 0; t < TM; ++t) {
@@ -265,7 +265,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     S[L.U0 + i] = (i < NQ && row) ? rhs[0] : 0.0;
     S[L.X0 + i] = mn ? 0.0 : tau_imp_i;
     S[L.XV + i] = mn ? 0.0 : tau_imp_i;
-    __syncthreads();
+    wave_sync();
 
     // ---------------------- 3. level-0 rows: Gamma_EE, targets b0, activities at x0
     // b0_c = G_c M^-1 J_t^T F_t = X_c . (J_t^T F_t), s0_c = X_c . x0 (lane c < m0);
@@ -308,7 +308,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         }
         s_i = S[L.X0 + j];
     }
-    __syncthreads();
+    wave_sync();
     const double nrm = kind != 0 ? sqrt(fmax(S[L.GM + ci * L.GS + ci], 1e-300)) : 1.0;
 
     // ------------------------------------ 5. dual active set in constraint space
@@ -324,7 +324,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     // the JointLimits box can empty per instance (a joint beyond its limit and moving outwards)
     const bool empty_box = a.joint_limits && __any(kind == 2 && ci >= m0 && lo > hi);
     gs.status = st0 != 0 ? st0 : (notspd ? 3 : ((a.limits_crossed || empty_box) ? 2 : 0));
-    __syncthreads();
+    wave_sync();
     const W1mGi pb{S, &L, m0, n, i, n};
     const GiVecs gv{L.VV, L.LV, L.RV, L.WV, L.AC, L.TT, L.TS};
     if (gs.status == 0) {
@@ -371,13 +371,13 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
                 if (r < m0 && i < m0) S[L.TT + r * L.TS + i] = t[r]; // T rows (lane c writes column c)
             if (i < m0) S[L.VV + i] = lo - s_i;                       // b0 - s_E
             S[L.AC + i] = (double)i;                                   // slot q = row q
-            __syncthreads();
+            wave_sync();
             const double w = i < m0 ? Trow.dot(S + L.VV, m0) : 0.0;
             S[L.LV + i] = w;
-            __syncthreads();
+            wave_sync();
             const double lm = i < m0 ? Tcol.dot(S + L.LV, m0) : 0.0; // lambda_E
             S[L.RV + i] = lm;
-            __syncthreads();
+            wave_sync();
             if (kind != 0) s_i += GA.dot(S + L.RV, m0);
             if (i < m0) {
                 gs.act = i;
@@ -387,7 +387,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
             }
             gs.k = m0;
             gs.iters = 1;
-            __syncthreads();
+            wave_sync();
         }
     }
     // the last solve's active bounds on top of the level-0 batch (dual_gi.h warm_extend)
@@ -396,7 +396,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
         (void)warm_extend<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, s_i, gs, wsg);
     }
     dual_gi<64>(pb, S, gv, i, Trow, Tcol, GA, kind, lo, hi, nrm, s_i, gs, a.max_iter);
-    __syncthreads();
+    wave_sync();
     int status = gs.status;
     if ((status == 2 || status == 3) && !R && !a.limits_crossed && !empty_box && !notspd) {
         // no step: level 0 is not attainable at b0 inside the limits; or the active set went
@@ -419,7 +419,7 @@ __device__ __forceinline__ void w1m_solve(const QppvmArgs &a, double *S, long b,
     if (a.integrate && !mn) { // qdd = M^-1 x = u_imp + (M^-1 G^T) lam_E + lam_B (refused without a joint task)
         S[L.RV + i] = i < gs.k ? gs.sgn * gs.lam : 0.0;
         S[L.AC + i] = (double)gs.act;
-        __syncthreads();
+        wave_sync();
         double u = S[L.U0 + i];
         for (int q = 0; q < gs.k; ++q) {
             const int c = (int)S[L.AC + q];
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
         const bool row = i < n;
         const int ic = row ? i : n - 1;
         const double h_i = row ? a.h[b * n + i] : 0.0;
-        __syncthreads(); // the previous instance's LDS is dead
+        wave_sync(); // the previous instance's LDS is dead
         double lo = -kInf, hi = kInf;
         if (row) torque_box(a, i, a.q[b * n + i], a.qd[b * n + i], h_i, lo, hi);
         const RepairOut ro = level0_repair<64, M0>(a, 0, b, i, true, lo, hi, false);
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
             ys[c] = g * ro.u;
         }
         isum_vec<64, M0>(ys);
-        __syncthreads(); // the repair's LDS is dead
+        wave_sync(); // the repair's LDS is dead
         R[RepairIn::LO + i] = ro.lo;
         R[RepairIn::HI + i] = ro.hi;
         if (i < M0) {
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
             for (int c = 0; c < M0; ++c) y = (c == i) ? ys[c] : y;
             R[RepairIn::YS + i] = y;
         }
-        __syncthreads();
+        wave_sync();
         w1m_solve<NQ, M0, TM>(a, smem, b, i, R, ro.it, ro.status, ro.l0inf);
     }
 }

@@ -70,6 +70,24 @@ __device__ __forceinline__ void lds_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Ordering of LDS accesses inside one-wave workgroups (round 6; every kernel of this library is one wave per
+// workgroup): the LDS unit executes one wave's DS instructions in issue order, so a lane's write is seen by another
+// lane's later read without a workgroup barrier, and only the compiler must keep the order. __syncthreads() also
+// waits for every outstanding memory access (s_waitcnt vmcnt(0) lgkmcnt(0)). WBQ_WAVE_SYNC = 0: __syncthreads()
+// (A/B). Used by block_gj and the contact-form / W1 = M kernels' LDS hand-offs.
+#ifndef WBQ_WAVE_SYNC
+#define WBQ_WAVE_SYNC 1
+#endif
+__device__ __forceinline__ void wave_sync()
+{
+#if WBQ_WAVE_SYNC
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    __syncthreads();
+#endif
+}
+
 // fast reciprocal / reciprocal square root: hardware estimate + one Newton step (~0.5 ulp)
 __device__ __forceinline__ double frcp(double x)
 {
@@ -558,7 +576,7 @@ __device__ __forceinline__ bool block_gj(double (&A)[NC], double (&rhs)[NR], int
     for (int kb = 0; kb < NC / BS; ++kb) {
         const int k = kb * BS;
         if (k < n) {
-            __syncthreads();
+            wave_sync();
             const double *pn = PN + (kb & 1) * NP * BS;
             const double *rh = RH + (kb & 1) * BS * RHS;
             double *pnn = PN + ((kb + 1) & 1) * NP * BS;
