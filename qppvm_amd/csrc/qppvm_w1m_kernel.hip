@@ -446,6 +446,11 @@ __global__ __launch_bounds__(64) void qppvm_w1m_kernel(const QppvmArgs a)
     w1m_solve<NQ, M0, TM>(a, smem, blockIdx.x, threadIdx.x, nullptr, 0, 0);
 }
 
+// LDS of the level-0 repair (level0_repair<64, M0>): only the QA region of the active-set layout -- the
+// Gauss-Jordan panel for A0, the 12-row BVLS slot matrix and the Q1 rows (64 rows of stride 65) -- so the repair
+// kernel reserves that, not the whole 64-lane active-set layout (101 KB: one block per CU; 34 KB: four)
+constexpr int kL0RepairLds = 64 * 65;
+
 // Level-0 repair for W1 = M: BVLS for y* and the pinned limits (level0_repair of the W1 = I
 // path, one instance per wave), then the W1 = M solve again with those.
 template <int NQ, int M0, int TM>
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(64) void qppvm_w1m_repair_kernel(const QppvmArgs a)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int i = threadIdx.x;
     const int n = a.n, m0 = a.m0;
-    const int ws = ActiveLayout<64>(a.ntasks, m0).SIZE;
+    const int ws = kL0RepairLds;
     const int wm = W1mLayout(n, a.ntasks, m0, NQ, 1 + M0).SIZE;
     double *R = smem + (ws > wm ? ws : wm);
     const int cnt = a.work[a.epoch * 2 + 1];
@@ -513,7 +518,7 @@ hipError_t launch_w1m_t(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
     const W1mLayout L(a.n, a.ntasks, a.m0, NQ, 1 + M0);
     if (L.ME > 64) return hipErrorInvalidValue;
     const size_t lds = sizeof(double) * L.SIZE;
-    const int ws = ActiveLayout<64>(a.ntasks, a.m0).SIZE;
+    const int ws = kL0RepairLds;
     const size_t lds2 = sizeof(double) * ((ws > L.SIZE ? ws : L.SIZE) + RepairIn::SIZE);
     if (a.prepare) {
         const hipError_t e = ensure_dynamic_lds((const void *)qppvm_w1m_kernel<NQ, M0, TM>, lds);
