@@ -268,14 +268,19 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     // temporaries spilled the fast path, 0 -> 428 B)
     constexpr bool kGivens = WBQ_GI_GIVENS != 0 && !MREG;
     const int n = a.n, m0 = a.m0;
-    const ActiveLayout<NP> L(a.ntasks, m0);
+    const ActiveLayout<NP> L(a.ntasks, m0, n);
     const int ic = i < n ? i : n - 1;
+    const bool lrow = i < L.NR; // (NP = 64: a lane past the layout's rows reads the zero row, writes nothing)
     WBQ_LAP_INIT; // (diagnostic build: cycles per phase of the loop, stamp slots 20-27, counts 13-14)
     // M rows (columns, coalesced); 64-bit addressing: the instances of a wave come from a work
     // list here, so no wave-uniform base exists for a buffer resource
     const double *Mb = a.M + b * n * n + ic;
     RowStore<NP, MREG> Mr;
-    Mr.bind(S + L.MA + i * RS);
+    Mr.bind(lrow ? S + L.MA + i * RS : S + L.ZR, lrow);
+    if constexpr (!MREG) {
+        S[L.ZR + i] = 0.0;
+        if (i == 0) S[L.ZR + NP] = 0.0;
+    }
     double mrow[NP];
 #pragma unroll
     for (int r = 0; r < NP; ++r) mrow[r] = Mb[(r < n ? r : n - 1) * n];
@@ -285,8 +290,9 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
 #pragma unroll
         for (int r = 0; r < NP; ++r) Mr.v[r] = mrow[r];
     } else {
+        if (lrow)
 #pragma unroll
-        for (int r = 0; r < NP; ++r) S[L.MA + i * RS + r] = mrow[r];
+            for (int r = 0; r < NP; ++r) S[L.MA + i * RS + r] = mrow[r];
     }
     double nrm2 = 0.0;
 #pragma unroll
@@ -295,7 +301,7 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
     S[L.D1 + NP + i] = 0.0;
     S[L.U + i] = u_i;
     RowStore<NP, MREG> Tr;
-    Tr.bind(S + L.TT + i * RS);
+    Tr.bind(lrow ? S + L.TT + i * RS : S + L.ZR, lrow);
     Tr.zero();
     int k = 0, q = m0;
     int act_p = -1, act_s = 0; // lane a < k: active inequality a (row index, sign)
@@ -339,7 +345,8 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
             const double zr = project_out<NP>(S, L, nj, on ? q : 0, i, npn * npn, on, zzr, n);
             const bool indep = zzr > 1e-16 * npn * npn;
             if (on && !indep && !skipdep) dep = true; // a dependent batch: start cold
-            const bool add = on && (indep || !skipdep);
+            if (on && (indep || !skipdep) && q >= L.NR) dep = true; // (the basis rows the layout holds: cold)
+            const bool add = on && (indep || !skipdep) && q < L.NR;
             double rr2 = 0.0;
             if (add && i < kk) rr2 = Tr.dot(S + L.D1 + m0, NP == 64 ? kk : NP);
             if (add) {
@@ -439,7 +446,8 @@ __device__ __forceinline__ double gi_solve(const QppvmArgs &a, double *S, long b
         int ci = i;
         iargmin<NP>(cand, ci);
         const double t1 = cand;
-        const double t2 = (zz > 1e-20 * npn * npn) ? -sp / zz : kInf;
+        // (q < NR: the basis has at most n rows; a candidate past the layout's rows is treated as dependent)
+        const double t2 = (zz > 1e-20 * npn * npn && q < L.NR) ? -sp / zz : kInf;
         bool rebuild = false;
         int cdrop = 0;
         if (go && t1 >= kInf && t2 >= kInf) {
@@ -629,7 +637,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
     constexpr int IPW = kWave / NP;
     constexpr int RS = NP + 1;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const ActiveLayout<NP> L(a.ntasks, a.m0, a.n); // (rows sized by n: launch_one's kNSized)
     const int sub = threadIdx.x / NP;
     const int i = threadIdx.x - sub * NP;
     double *S = smem + sub * L.SIZE;
@@ -656,7 +664,7 @@ __global__ __launch_bounds__(64, NP == 32 ? 2 : 1) void qppvm_active_kernel(cons
         __syncthreads(); // the previous instance's LDS is dead
 #pragma unroll
         for (int c = 0; c < NP; ++c)
-            S[L.QA + c * RS + i] = (valid && c < M0 && c < a.m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
+            if (c < L.NR) S[L.QA + c * RS + i] = (valid && c < M0 && c < a.m0) ? qs[(c < M0 ? c : 0) * NP + i] : 0.0;
         int status = 0, iters = 0;
         bool infeasible = false;
         WBQ_STAMP(6);
@@ -738,7 +746,7 @@ __device__ __forceinline__ void repair_instance(const QppvmArgs &a, double *S, l
     // point is degenerate by construction -- the pins and G u = y* are dependent -- and could end
     // with "no step", status 2: the config-4 rollouts once did, scripts/diag_mpc.py.)
     const bool uniq = ro.unique;
-    const ActiveLayout<NP> L(a.ntasks, a.m0);
+    const ActiveLayout<NP> L(a.ntasks, a.m0, n); // (gi_solve's layout: u at L.U)
     double x_i = ro.x;
     // the dual active set starts from the BVLS point's bound set in one batch (gi_solve's warm start:
     // kept only if independent and dual feasible, else cold; the path changes, never the solution). The
@@ -1827,10 +1835,14 @@ __global__ __launch_bounds__(64, WBQ_ROLL_W) void qppvm_rollout_kernel(const Qpp
 }
 
 template <int NP, typename Lay, typename K>
-hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t stream)
+hipError_t launch_one(K kern, const QppvmArgs &a, unsigned grid, hipStream_t stream, bool nsized = false)
 {
     constexpr int IPW = kWave / NP;
-    const size_t lds = sizeof(double) * Lay(a.ntasks, a.m0).SIZE * IPW;
+    // nsized: the 64-lane active-set kernel's layout with its rows sized by n (ActiveLayout)
+    int size = Lay(a.ntasks, a.m0).SIZE;
+    if constexpr (std::is_same_v<Lay, ActiveLayout<NP>>)
+        if (nsized) size = ActiveLayout<NP>(a.ntasks, a.m0, a.n).SIZE;
+    const size_t lds = sizeof(double) * size * IPW;
     if (a.prepare) return ensure_dynamic_lds((const void *)kern, lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, a);
     return hipGetLastError();
@@ -1903,12 +1915,12 @@ hipError_t launch_np(const QppvmArgs &a, hipStream_t stream, hipEvent_t mid)
         return launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
     } else {
         const unsigned g0 = follow_blocks(a.fg.est[0], IPW, kFollowGrid, a.B);
-        e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, g0, stream);
+        e = launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0>, a, g0, stream, true);
         if (e != hipSuccess) return e;
         e = launch_one<NP, ActiveLayout<NP>>(qppvm_repair_kernel<NP, M0>, a, g1, stream);
         if (e != hipSuccess || !(a.handback || a.prepare)) return e;
         // the repaired instances' dual active sets (work list 2), sized like the repair grid
-        return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0, true>, a, g1, stream);
+        return launch_one<NP, ActiveLayout<NP>>(qppvm_active_kernel<NP, M0, true>, a, g1, stream, true);
     }
 }
 

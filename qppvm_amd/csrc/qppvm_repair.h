@@ -11,13 +11,18 @@ template <int NP>
 struct ActiveLayout {
     static constexpr bool MREG = (NP == 32); // M rows and T rows in VGPRs (else in LDS)
     static constexpr int RS = NP + 1;
-    int QA, MA, TT, U, D1, D1B, NV, BC, SIZE;
-    __host__ __device__ ActiveLayout(int, int)
+    int NR, QA, MA, TT, ZR, U, D1, D1B, NV, BC, SIZE;
+    // n (NP = 64, round 6): the three row regions hold the rows an n-joint instance can use -- n rounded up to 8,
+    // Q1^T's basis has at most n rows, M's and T's rows past n are padding -- instead of 64 (n = 39: 40 rows,
+    // 101 -> 64 KB, two instances per CU instead of one); the lanes past NR read a zero row (ZR) and write nothing
+    __host__ __device__ ActiveLayout(int, int, int n = NP)
     {
-        QA = 0;                           // Q1^T rows [NP][RS]
-        MA = QA + NP * RS;                // M rows (NP == 64)
-        TT = MA + (MREG ? 0 : NP * RS);   // T = R_II^-1 rows (NP == 64)
-        U = TT + (MREG ? 0 : NP * RS);    // u
+        NR = MREG ? NP : (n < NP ? ((n + 7) & ~7) : NP);
+        QA = 0;                           // Q1^T rows [NR][RS]
+        MA = QA + NR * RS;                // M rows (NP == 64)
+        TT = MA + (MREG ? 0 : NR * RS);   // T = R_II^-1 rows (NP == 64)
+        ZR = TT + (MREG ? 0 : NR * RS);   // a zero row (NP == 64)
+        U = ZR + (MREG ? 0 : RS + 1);     // u
         D1 = U + NP;                      // d1 = Q1^T n_p, zero-padded to 2 NP
         D1B = D1 + 2 * NP;                // second Gram-Schmidt pass
         NV = D1B + NP;                    // n_p

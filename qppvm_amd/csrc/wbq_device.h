@@ -139,7 +139,7 @@ struct RowStore;
 template <int NP>
 struct RowStore<NP, true> {
     double v[NP];
-    __device__ void bind(double *) {}
+    __device__ void bind(double *, bool = true) {}
     __device__ void zero()
     {
 #pragma unroll
@@ -173,12 +173,21 @@ struct RowStore<NP, true> {
 template <int NP>
 struct RowStore<NP, false> {
     double *row;
-    __device__ void bind(double *p) { row = p; }
+    bool live = true; // false: a lane past the layout's rows, bound to a zero row: reads 0, writes nothing
+    __device__ void bind(double *p, bool lv = true)
+    {
+        row = p;
+        live = lv;
+    }
     __device__ void zero()
     {
-        for (int j = 0; j < NP; ++j) row[j] = 0.0;
+        if (live)
+            for (int j = 0; j < NP; ++j) row[j] = 0.0;
     }
-    __device__ void set(int c, double x) { row[c] = x; }
+    __device__ void set(int c, double x)
+    {
+        if (live) row[c] = x;
+    }
     __device__ double get(int c) const { return row[c]; }
     __device__ double at(int c) const { return row[c]; }
     // chunks of 8 independent LDS reads into four accumulators instead of a chain of cnt dependent
