@@ -104,6 +104,22 @@ def test_random_vs_oracle_active_bounds(wbq_mod, oracle_lib, n, frac):
     assert it.max() > 0  # the active set really moved
 
 
+@pytest.mark.parametrize("n,frac", [(33, 0.5), (40, 0.5), (40, 0.8), (47, 0.6), (64, 0.6)])
+def test_saturated_sets_n_sized_layout(wbq_mod, oracle_lib, n, frac):
+    """n > 32 with most limits active: the 64-lane active-set kernel's layout holds NR = n rounded up to 8 basis / M / T
+    rows (qppvm_repair.h ActiveLayout; n = 40: NR = n, the basis can fill every row). Statuses equal to the oracle's,
+    tau within TOL where it solves."""
+    inp = qppvm_instances(QPPVMProblem(n=n), 48, seed=700 + n)
+    prob = calibrated({}, n, inp, oracle_lib, frac)
+    tau_r, st_r, _ = oracle_lib.qppvm_batch(prob, inp)
+    tau, st, it = gpu_solve(wbq_mod, prob, inp)
+    np.testing.assert_array_equal(st, st_r)
+    ok = st_r == 0
+    assert ok.sum() >= len(st) // 2
+    assert rel_err(tau[ok], tau_r[ok]) <= TOL, rel_err(tau[ok], tau_r[ok])
+    assert it.max() > 0
+
+
 def test_select_task_mode_and_six_rows(wbq_mod, oracle_lib):
     for kw in (dict(select_mode=SELECT_TASK), dict(row_mask=(0x3F, 0x3F)), dict(row_mask=(0x5, 0x38))):
         prob = QPPVMProblem(n=30, tau_max=1e7, **kw)
